@@ -1,0 +1,173 @@
+"""ctypes wrapper over oracle/liboracle.so — the CPU restatement used as the parity checker.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package (cryptmpi_2022_amd/).  See oracle/oracle.h for
+what each function restates and the reference file:line it follows.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build() -> None:
+    import subprocess
+
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        sig = {
+            "orc_aes128_expand": [P, P],
+            "orc_aes128_encrypt": [P, P, P],
+            "orc_aes128_decrypt": [P, P, P],
+            "orc_aes128_ecb": [P, P, P, S],
+            "orc_gf128_mul": [P, P, P],
+            "orc_ghash": [P, P, S, P, S, P],
+            "orc_gcm_seal": [P, P, S, P, S, P, S, P],
+            "orc_gcm_open": [P, P, S, P, S, P, S, P],
+            "orc_gcm_seal_batch": [P, P, S, P, S, P, S, S, S, I],
+            "orc_gcm_open_batch": [P, P, S, P, S, P, S, S, S, P, I],
+            "orc_ctr128_xor": [P, P, P, P, S],
+            "orc_ctr128_xor_mt": [P, P, P, P, S, I],
+            "orc_iv_count": [P, ctypes.c_ulong],
+            "orc_iv_count_out": [P, ctypes.c_ulong, P],
+            "orc_ocb_seal": [P, P, S, P, S, P, S, P],
+            "orc_ocb_open": [P, P, S, P, S, P, S, P],
+            "orc_ocb_seal_batch": [P, P, S, P, S, P, S, S, S, I],
+            "orc_nonce602": [P, ctypes.c_uint8, ctypes.c_uint32],
+            "orc_header600": [P, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_uint32],
+        }
+        for name, args in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int if name in ("orc_gcm_seal", "orc_gcm_open", "orc_ocb_seal", "orc_ocb_open") else None
+        _lib = L
+    return _lib
+
+
+def _buf(b) -> ctypes.Array:
+    return (ctypes.c_uint8 * max(1, len(b))).from_buffer_copy(bytes(b) or b"\0")
+
+
+def _ptr(a: np.ndarray) -> int:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+# ---------------------------------------------------------------- single-message API
+def aes128_encrypt_block(key: bytes, block: bytes) -> bytes:
+    rk = (ctypes.c_uint8 * 176)()
+    out = (ctypes.c_uint8 * 16)()
+    lib().orc_aes128_expand(_buf(key), rk)
+    lib().orc_aes128_encrypt(rk, _buf(block), out)
+    return bytes(out)
+
+
+def aes128_decrypt_block(key: bytes, block: bytes) -> bytes:
+    rk = (ctypes.c_uint8 * 176)()
+    out = (ctypes.c_uint8 * 16)()
+    lib().orc_aes128_expand(_buf(key), rk)
+    lib().orc_aes128_decrypt(rk, _buf(block), out)
+    return bytes(out)
+
+
+def ecb_encrypt(key: bytes, data: bytes) -> bytes:
+    assert len(data) % 16 == 0
+    out = (ctypes.c_uint8 * max(1, len(data)))()
+    lib().orc_aes128_ecb(_buf(key), _buf(data), out, len(data) // 16)
+    return bytes(out)[: len(data)]
+
+
+def gf128_mul(x: bytes, y: bytes) -> bytes:
+    out = (ctypes.c_uint8 * 16)()
+    lib().orc_gf128_mul(_buf(x), _buf(y), out)
+    return bytes(out)
+
+
+def gcm_seal(key: bytes, nonce: bytes, pt: bytes, aad: bytes = b"") -> bytes:
+    out = (ctypes.c_uint8 * (len(pt) + 16))()
+    ok = lib().orc_gcm_seal(_buf(key), _buf(nonce), len(nonce), _buf(aad), len(aad), _buf(pt), len(pt), out)
+    assert ok == 1
+    return bytes(out)
+
+
+def gcm_open(key: bytes, nonce: bytes, ct_tag: bytes, aad: bytes = b""):
+    """Returns plaintext bytes, or None on authentication failure."""
+    out = (ctypes.c_uint8 * max(1, len(ct_tag) - 16))()
+    ok = lib().orc_gcm_open(_buf(key), _buf(nonce), len(nonce), _buf(aad), len(aad), _buf(ct_tag), len(ct_tag), out)
+    return bytes(out)[: len(ct_tag) - 16] if ok else None
+
+
+def ctr_xor(key: bytes, ctr0: bytes, data: bytes) -> bytes:
+    out = (ctypes.c_uint8 * max(1, len(data)))()
+    lib().orc_ctr128_xor(_buf(key), _buf(ctr0), _buf(data), out, len(data))
+    return bytes(out)[: len(data)]
+
+
+def iv_count(iv: bytes, cter: int) -> bytes:
+    b = _buf(iv)
+    lib().orc_iv_count(b, cter & 0xFFFFFFFFFFFFFFFF)
+    return bytes(b)
+
+
+def ocb_seal(key: bytes, nonce: bytes, pt: bytes, aad: bytes = b"") -> bytes:
+    out = (ctypes.c_uint8 * (len(pt) + 16))()
+    ok = lib().orc_ocb_seal(_buf(key), _buf(nonce), len(nonce), _buf(aad), len(aad), _buf(pt), len(pt), out)
+    assert ok == 1
+    return bytes(out)
+
+
+def ocb_open(key: bytes, nonce: bytes, ct_tag: bytes, aad: bytes = b""):
+    out = (ctypes.c_uint8 * max(1, len(ct_tag) - 16))()
+    ok = lib().orc_ocb_open(_buf(key), _buf(nonce), len(nonce), _buf(aad), len(aad), _buf(ct_tag), len(ct_tag), out)
+    return bytes(out)[: len(ct_tag) - 16] if ok else None
+
+
+def nonce602(flag: bytes, seg: int) -> bytes:
+    b = (ctypes.c_uint8 * 12)()
+    lib().orc_nonce602(b, flag[0], seg)
+    return bytes(b)
+
+
+# ---------------------------------------------------------------- batch API (numpy, host memory)
+def gcm_seal_batch(key: bytes, nonces: np.ndarray, pt: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    """nonces: (N,12) u8; pt: (N,n) u8 → (N, n+16) u8 (ct || tag)."""
+    N, n = pt.shape
+    out = np.empty((N, n + 16), dtype=np.uint8)
+    lib().orc_gcm_seal_batch(_buf(key), _ptr(nonces), nonces.strides[0], _ptr(pt), pt.strides[0], _ptr(out), out.strides[0], n, N, nthreads)
+    return out
+
+
+def gcm_open_batch(key: bytes, nonces: np.ndarray, ct_tag: np.ndarray, nthreads: int = 0):
+    N, m = ct_tag.shape
+    n = m - 16
+    out = np.empty((N, n), dtype=np.uint8)
+    status = np.empty(N, dtype=np.int32)
+    lib().orc_gcm_open_batch(_buf(key), _ptr(nonces), nonces.strides[0], _ptr(ct_tag), ct_tag.strides[0], _ptr(out), max(1, out.strides[0]), n, N, _ptr(status), nthreads)
+    return out, status
+
+
+def ocb_seal_batch(key: bytes, nonces: np.ndarray, pt: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    N, n = pt.shape
+    out = np.empty((N, n + 16), dtype=np.uint8)
+    lib().orc_ocb_seal_batch(_buf(key), _ptr(nonces), nonces.strides[0], _ptr(pt), pt.strides[0], _ptr(out), out.strides[0], n, N, nthreads)
+    return out
+
+
+def ctr_xor_mt(key: bytes, ctr0: bytes, data: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    out = np.empty_like(data)
+    lib().orc_ctr128_xor_mt(_buf(key), _buf(ctr0), _ptr(data), _ptr(out), data.nbytes, nthreads)
+    return out
