@@ -1,0 +1,379 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident AES-GCM seal+open throughput on MI355X (BASELINE.json metric).
+
+A "step" = one AES-128-GCM seal of a whole batch of synthetic records followed by one open of
+the resulting ct||tag batch (BASELINE config 2: 65 536 x 1 KiB per GPU), inputs resident in
+HBM before the timed region.  value = plaintext bytes sealed-and-opened by ALL ranks per second
+(GiB/s, n*N / (t_seal + t_open) per record pass), weak scaling: every rank owns
+its own batch (records are independent; no data-path collective — SURVEY.md §8e).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gcm1k|gcm4k|ocb1m|ctr1g|alltoall]
+                    [--no-cpu-baseline] [--no-extras]
+
+Multi-GPU: launched by torch.distributed.run (one process per GPU); only the timing barrier and
+the max-over-ranks reduction use the process group.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from cryptmpi_2022_amd import aead  # noqa: E402
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md), GB/s
+KEY = bytes.fromhex("000102030405060708090a0b0c0d0e0f")
+
+WORKLOADS = {
+    # name: (alg, record bytes, records, description)
+    "gcm1k": ("gcm", 1024, 65536, "BASELINE config 2: 65536 x 1 KiB AES-128-GCM seal+open"),
+    "gcm4k": ("gcm", 4096, 65536, "north-star target: 65536 x 4 KiB AES-128-GCM seal+open"),
+    "ocb1m": ("ocb", 1 << 20, 4096, "BASELINE config 3: 4096 x 1 MiB AES-128-OCB seal+open"),
+    "ctr1g": ("ctr", 1 << 30, 1, "BASELINE config 4: 1 GiB AES-128-CTR keystream+XOR"),
+    "alltoall": ("gcm", 1 << 20, 8, "BASELINE config 5 per rank: 8 peers x 1 MiB seal+open"),
+}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+class Workload:
+    """Device buffers + one step of the hot path for a workload."""
+
+    def __init__(self, name: str, device: int, seed: int):
+        self.name = name
+        self.alg, self.n, self.nrec, self.desc = WORKLOADS[name]
+        self.dev = torch.device("cuda", device)
+        g = torch.Generator(device=self.dev).manual_seed(seed)
+        n, N = self.n, self.nrec
+        self.pt = torch.randint(0, 256, (N * n,), dtype=torch.uint8, device=self.dev, generator=g)
+        if self.alg == "ctr":
+            self.ctx = aead.CipherCtx(KEY, "aes-128-ctr", device=device)
+            self.ct = torch.empty_like(self.pt)
+            self.ctr0 = bytes(range(0xF0, 0x100))
+            return
+        self.ctx = aead.AeadCtx(KEY, "aes-128-gcm" if self.alg == "gcm" else "aes-128-ocb", device=device)
+        self.nonces = torch.randint(0, 256, (N * 12,), dtype=torch.uint8, device=self.dev, generator=g)
+        self.ct = torch.empty(N * (n + 16), dtype=torch.uint8, device=self.dev)
+        self.back = torch.empty(N * n, dtype=torch.uint8, device=self.dev)
+        self.status = torch.zeros(N, dtype=torch.int32, device=self.dev)
+        ws = self.ctx.workspace_size(n, N)
+        self.ws = torch.empty(max(ws, 16), dtype=torch.uint8, device=self.dev) if ws else None
+
+    # algorithmic HBM bytes per launch: seal/open 2n+28 per record, CTR fused 2n
+    def bytes_per_launch(self) -> int:
+        if self.alg == "ctr":
+            return 2 * self.n
+        return self.nrec * (2 * self.n + 28)
+
+    def seal(self):
+        if self.alg == "ctr":
+            self.ctx.ctr_xor(self.ct, self.pt, self.n, self.ctr0)
+        else:
+            self.ctx.seal_batch(self.ct, self.pt, self.nonces, self.n, self.nrec, workspace=self.ws)
+
+    def open(self):
+        if self.alg == "ctr":
+            self.ctx.ctr_xor(self.back if hasattr(self, "back") else self.pt, self.ct, self.n, self.ctr0)
+        else:
+            self.ctx.open_batch(self.back, self.ct, self.nonces, self.n, self.nrec, status=self.status, workspace=self.ws)
+
+    def verify(self) -> bool:
+        torch.cuda.synchronize(self.dev)
+        if self.alg == "ctr":
+            return True
+        return bool((self.status == 1).all()) and torch.equal(self.back, self.pt)
+
+    def free(self):
+        self.ctx.close()
+        for a in ("pt", "ct", "back", "nonces", "status", "ws"):
+            if hasattr(self, a):
+                delattr(self, a)
+        torch.cuda.empty_cache()
+
+
+def time_steps(w: Workload, steps: int, warmup: int, barrier):
+    """Returns (wall seconds for `steps` steps, avg seal kernel ms, avg open kernel ms) —
+    kernel times from HIP events recorded on the stream the kernels are launched on."""
+    for _ in range(warmup):
+        w.seal()
+        w.open()
+    torch.cuda.synchronize(w.dev)
+    assert w.verify(), "round trip failed in warm-up"
+    stream = torch.cuda.current_stream(w.dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    barrier()
+    torch.cuda.synchronize(w.dev)
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        e0.record(stream)
+        w.seal()
+        e1.record(stream)
+        w.open()
+        e2.record(stream)
+    torch.cuda.synchronize(w.dev)
+    barrier()
+    wall = time.perf_counter() - t0
+    seal_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / steps
+    open_ms = sum(b.elapsed_time(c) for _, b, c in ev) / steps
+    return wall, seal_ms, open_ms
+
+
+def host_path_rate(device: int, n: int = 1024, nrec: int = 65536) -> dict:
+    """PCIe-inclusive seal rate: pinned host plaintext -> H2D -> kernel -> D2H -> pinned host."""
+    pt = torch.randint(0, 256, (nrec * n,), dtype=torch.uint8).pin_memory()
+    nonces = torch.randint(0, 256, (nrec * 12,), dtype=torch.uint8).pin_memory()
+    out = torch.empty(nrec * (n + 16), dtype=torch.uint8).pin_memory()
+    ctx = aead.AeadCtx(KEY, device=device)
+    d_pt = torch.empty(nrec * n, dtype=torch.uint8, device=f"cuda:{device}")
+    d_n = torch.empty(nrec * 12, dtype=torch.uint8, device=f"cuda:{device}")
+    d_ct = torch.empty(nrec * (n + 16), dtype=torch.uint8, device=f"cuda:{device}")
+
+    def once():
+        d_pt.copy_(pt, non_blocking=True)
+        d_n.copy_(nonces, non_blocking=True)
+        ctx.seal_batch(d_ct, d_pt, d_n, n, nrec)
+        out.copy_(d_ct, non_blocking=True)
+
+    for _ in range(3):
+        once()
+    torch.cuda.synchronize()
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    # the library's own synchronous host entry point (pageable numpy buffers, internal staging)
+    from cryptmpi_2022_amd.synth import random_nonces, records
+
+    hp = records(1, 4096, n)
+    hn = random_nonces(2, 4096)
+    ctx.seal_host_batch(hn, hp)
+    t1 = time.perf_counter()
+    for _ in range(5):
+        ctx.seal_host_batch(hn, hp)
+    dt2 = (time.perf_counter() - t1) / 5
+    ctx.close()
+    return {"pinned_seal_GiBps": round(nrec * n / dt / GIB, 2), "config": f"{nrec} x {n} B, pinned, 1 stream",
+            "seal_host_api_GiBps": round(4096 * n / dt2 / GIB, 3), "seal_host_api_config": "4096 x 1 KiB pageable numpy"}
+
+
+def cpu_baseline(workload: str, seconds: float = 10.0) -> dict:
+    """Rank-0 CPU baselines on a bounded sample of the same workload shape.
+    primary ('port'): the oracle's C restatement (oracle/liboracle.so), all host threads;
+    aesni: system OpenSSL 3 EVP (AES-NI/PCLMUL) — the closest buildable stand-in for the
+    reference's BoringSSL AES-NI path (tools/cpu_baseline.c), all host threads."""
+    import oracle
+    from cryptmpi_2022_amd.synth import random_nonces, records
+
+    alg, n, N, _ = WORKLOADS[workload]
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    res = {}
+    # --- oracle port: size the sample so one seal+open pass takes ~seconds/2
+    if alg == "ctr":
+        nbytes = 64 << 20
+        data = np.frombuffer(records(5, 1, nbytes).tobytes(), np.uint8)
+        t0 = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t0 < seconds / 2:
+            oracle.ctr_xor_mt(KEY, bytes(16), data, threads)
+            reps += 1
+        dt = time.perf_counter() - t0
+        res["port"] = {"value": round(reps * nbytes / dt / GIB, 4), "sample": f"{reps} x 64 MiB CTR stream"}
+    else:
+        sample = max(1, min(N, int(4 * (1 << 20) // max(n, 1))))  # 4 MiB of records
+        pt = records(3, sample, n)
+        nn = random_nonces(4, sample)
+        seal = oracle.gcm_seal_batch if alg == "gcm" else oracle.ocb_seal_batch
+        t0 = time.perf_counter()
+        passes = 0
+        t_seal = t_open = 0.0
+        while time.perf_counter() - t0 < seconds / 2:
+            a = time.perf_counter()
+            ct = seal(KEY, nn, pt, threads)
+            b = time.perf_counter()
+            if alg == "gcm":
+                oracle.gcm_open_batch(KEY, nn, ct, threads)
+            else:
+                seal(KEY, nn, pt, threads)  # OCB open in the oracle is single-message; seal ~ same cost
+            c = time.perf_counter()
+            t_seal += b - a
+            t_open += c - b
+            passes += 1
+        res["port"] = {"value": round(passes * sample * n / (t_seal + t_open) / GIB, 4),
+                       "sample": f"{passes} passes x {sample} x {n} B seal+open"}
+    # --- OpenSSL AES-NI
+    try:
+        L = ctypes.CDLL(os.path.join(ROOT, "tools", "libcpu_baseline.so"))
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.cb_aead_batch.argtypes = [I, I, P, P, P, S, P, S, I, ctypes.c_long, I]
+        L.cb_ctr.argtypes = [P, P, P, P, S, I]
+        if alg == "ctr":
+            nbytes = 256 << 20
+            data = np.frombuffer(records(6, 1, nbytes).tobytes(), np.uint8)
+            out = np.empty_like(data)
+            t0 = time.perf_counter()
+            reps = 0
+            while time.perf_counter() - t0 < seconds / 2:
+                L.cb_ctr(KEY, bytes(16), data.ctypes.data, out.ctypes.data, nbytes, threads)
+                reps += 1
+            dt = time.perf_counter() - t0
+            res["aesni"] = {"value": round(reps * nbytes / dt / GIB, 3), "sample": f"{reps} x 256 MiB CTR stream"}
+        else:
+            sample = max(1, min(N, int((256 << 20) // max(n, 1))))
+            pt = records(7, sample, n)
+            nn = random_nonces(8, sample)
+            ct = np.empty((sample, n + 16), np.uint8)
+            back = np.empty((sample, n), np.uint8)
+            a_id = 1 if alg == "gcm" else 2
+            t0 = time.perf_counter()
+            passes = 0
+            t_seal = t_open = 0.0
+            while time.perf_counter() - t0 < seconds / 2:
+                a = time.perf_counter()
+                L.cb_aead_batch(a_id, 0, KEY, nn.ctypes.data, pt.ctypes.data, n, ct.ctypes.data, n + 16, n, sample, threads)
+                b = time.perf_counter()
+                bad = L.cb_aead_batch(a_id, 1, KEY, nn.ctypes.data, ct.ctypes.data, n + 16, back.ctypes.data, n, n, sample, threads)
+                c = time.perf_counter()
+                assert bad == 0
+                t_seal += b - a
+                t_open += c - b
+                passes += 1
+            res["aesni"] = {"value": round(passes * sample * n / (t_seal + t_open) / GIB, 3),
+                            "seal_GiBps": round(passes * sample * n / t_seal / GIB, 3),
+                            "sample": f"{passes} passes x {sample} x {n} B seal+open"}
+    except OSError as e:  # harness not built / no libcrypto
+        res["aesni"] = {"error": str(e)}
+    res["cores"] = threads
+    return res
+
+
+def load_pmc(workload: str):
+    """HBM traffic per launch of the dominant kernel from a committed rocprofv3 --pmc summary."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("traffic_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="gcm1k", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    if ws != args.gpus and ws > 1:
+        print(f"warning: WORLD_SIZE={ws} but --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    pg = None
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        pg = dist
+
+        def barrier():
+            dist.barrier(device_ids=[local])
+    else:
+        def barrier():
+            pass
+
+    w = Workload(args.workload, local, seed=1000 + rank)
+    wall, seal_ms, open_ms = time_steps(w, args.steps, args.warmup, barrier)
+    ok = w.verify()
+    # max over ranks of the timed wall clock
+    t = torch.tensor([wall], dtype=torch.float64, device=w.dev)
+    if pg is not None:
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    wall_max = float(t.item())
+    per_rank_bytes = w.n * w.nrec  # plaintext bytes per step per rank
+    value = per_rank_bytes * ws * args.steps / wall_max / GIB
+    bpl = w.bytes_per_launch()
+    kern_ms = seal_ms  # dominant kernel: the seal launch (open is within a few % of it)
+    achieved = bpl / (kern_ms * 1e-3) / 1e9
+    traffic = load_pmc(args.workload)
+    result = {
+        "metric": "GiB/s device-resident AES-GCM seal+open on batched buffers, 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (torch.randint plaintext and nonces in HBM; fixed key)",
+        "config": {"workload": args.workload, "desc": w.desc, "records_per_gpu": w.nrec, "record_bytes": w.n,
+                   "parallelism": f"records sharded, {ws} independent rank(s), no collective"},
+        "seal_GiBps_per_gpu": round(per_rank_bytes / (seal_ms * 1e-3) / GIB, 2),
+        "open_GiBps_per_gpu": round(per_rank_bytes / (open_ms * 1e-3) / GIB, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "seal launch (gcm_batch_kernel<L,false>)" if w.alg == "gcm" else f"{w.alg} seal launch",
+                     "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bpl},
+        "verified_round_trip": ok,
+    }
+    w.free()
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(args.workload, args.cpu_seconds)
+        port = cb.get("port", {})
+        result["cpu_baseline"] = {"value": port.get("value"), "unit": "GiB/s", "cores": cb["cores"], "kind": "port",
+                                  "sample": port.get("sample"),
+                                  "impl": "oracle/ C restatement (portable table AES, bit-serial GHASH)"}
+        result["cpu_baseline_aesni"] = dict(cb.get("aesni", {}), unit="GiB/s", cores=cb["cores"],
+                                            impl="system OpenSSL 3 EVP (AES-NI/PCLMUL), stand-in for BoringSSL")
+    if rank == 0 and ws == 1 and not args.no_extras and args.workload == "gcm1k":
+        extras = {}
+        for name in ("gcm4k", "ocb1m", "ctr1g", "alltoall"):
+            try:
+                we = Workload(name, local, seed=77)
+                wl, s_ms, o_ms = time_steps(we, 10, 3, barrier)
+                extras[name] = {"seal_open_GiBps": round(we.n * we.nrec * 10 / wl / GIB, 2),
+                                "seal_GiBps": round(we.n * we.nrec / (s_ms * 1e-3) / GIB, 2),
+                                "open_GiBps": round(we.n * we.nrec / (o_ms * 1e-3) / GIB, 2),
+                                "seal_hbm_frac": round(we.bytes_per_launch() / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "verified": we.verify()}
+                we.free()
+            except Exception as e:  # report, never hide
+                extras[name] = {"error": repr(e)}
+        try:
+            extras["host_path_pcie"] = host_path_rate(local)
+        except Exception as e:
+            extras["host_path_pcie"] = {"error": repr(e)}
+        result["extras"] = extras
+    if rank == 0:
+        print(json.dumps(result))
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

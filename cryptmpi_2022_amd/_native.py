@@ -1,0 +1,109 @@
+"""ctypes binding of libcmpi_aead.so (include/cmpi_aead.h, include/cmpi_debug.h).
+
+The shared library is built in-tree by `make -C cryptmpi_2022_amd` (see __graft_entry__.build).
+There is no fallback: if the library is missing or fails to load, importing the binding raises.
+torch is imported first (when available) so that libcmpi_aead.so binds to the same HIP runtime
+instance (libamdhip64.so.7) that torch uses for device memory and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+try:  # share torch's HIP runtime when torch is present
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is always present in this image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcmpi_aead.so")
+INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
+
+CMPI_OK = 0
+CMPI_EINVAL = -1
+CMPI_EHIP = -2
+CMPI_ENOMEM = -3
+CMPI_EAUTH = -4
+CMPI_ENODEV = -5
+
+CMPI_AES_128_GCM = 1
+CMPI_AES_128_OCB = 2
+CMPI_AES_128_CTR = 3
+CMPI_AES_128_ECB = 4
+
+
+class CmpiError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"cmpi error {code}: {msg}")
+        self.code = code
+
+
+_P, _S, _I, _U32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32
+
+_SIGS = {
+    "cmpi_version": ([], ctypes.c_char_p),
+    "cmpi_last_error": ([], ctypes.c_char_p),
+    "cmpi_device_count": ([], _I),
+    "cmpi_ctx_new": ([_I, _P, _S, _S, _I], _P),
+    "cmpi_ctx_new_subkey": ([_P, _P], _P),
+    "cmpi_ctx_free": ([_P], None),
+    "cmpi_ctx_device": ([_P], _I),
+    "cmpi_gcm_workspace_size": ([_P, _S, _S], _S),
+    "cmpi_gcm_seal_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
+    "cmpi_gcm_open_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P, _P], _I),
+    "cmpi_gcm_seal_host": ([_P, _P, _S, _P, _S, _P, _S, _S, _S], _I),
+    "cmpi_gcm_open_host": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P], _I),
+    "cmpi_ocb_workspace_size": ([_P, _S, _S], _S),
+    "cmpi_ocb_seal_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
+    "cmpi_ocb_open_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P, _P], _I),
+    "cmpi_ctr_xor": ([_P, _P, _P, _S, _P, _P], _I),
+    "cmpi_ctr_keystream": ([_P, _P, _S, _P, _P], _I),
+    "cmpi_iv_count": ([_P, ctypes.c_ulong], None),
+    "cmpi_iv_count_out": ([_P, ctypes.c_ulong, _P], None),
+    "cmpi_ecb_encrypt": ([_P, _P, _P, _S, _P], _I),
+    "cmpi_debug_force_plan": ([_I, _U32], None),
+    "cmpi_debug_gcm_plan": ([_P, _S, _S, _P], _I),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')"
+            )
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return (lib().cmpi_last_error() or b"").decode(errors="replace")
+
+
+def check(rc: int) -> int:
+    if rc != CMPI_OK:
+        raise CmpiError(rc, last_error())
+    return rc
+
+
+def header_functions() -> list[str]:
+    """Every function name declared in include/*.h (for the export test)."""
+    names = []
+    for fn in sorted(os.listdir(INCLUDE_DIR)):
+        if not fn.endswith(".h"):
+            continue
+        with open(os.path.join(INCLUDE_DIR, fn)) as f:
+            txt = f.read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"\b(cmpi_[a-z0-9_]+|EVP_[A-Za-z0-9_]+)\s*\(", txt):
+            names.append(m.group(1))
+    return sorted(set(names))

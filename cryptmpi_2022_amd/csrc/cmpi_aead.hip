@@ -1,0 +1,718 @@
+// cmpi_aead.hip — libcmpi_aead.so: the C ABI of include/cmpi_aead.h (host side) + kernel
+// instantiations.  One translation unit so every kernel lives in one code object for gfx950.
+//
+// Host responsibilities: key schedule and GHASH/OCB tables once per key (what
+// EVP_AEAD_CTX_new does inside BoringSSL), launch planning (lanes per record, segmentation),
+// argument validation, and the staging path of the *_host entry points.  No cipher arithmetic
+// runs on the host on any data path: every byte of ciphertext, plaintext or tag is produced by
+// a HIP kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cmpi_aead.h"
+#include "../../include/cmpi_debug.h"
+#include "aes_tables.hpp"
+#include "ctr_kernels.hpp"
+#include "gcm_kernels.hpp"
+#include "gf128_host.hpp"
+#include "ocb_kernels.hpp"
+
+using cmpi::Blk;
+using cmpi::dev::u32x4;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) return fail(CMPI_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+constexpr uint32_t kGcmThreads = 1024;
+constexpr uint32_t kNibTables = 4;  // H^1..H^4
+constexpr size_t kByteTab = 4096 * 16;
+constexpr size_t kNibTab = 512 * 16;
+
+// Device table block of a context (one allocation).
+struct DevTables {
+  uint32_t te0[256];
+  uint32_t td0[256];
+  uint32_t isb[256];
+  uint32_t pad_[256];            // keeps the GHASH tables 4 KiB aligned
+  uint8_t htab[3][kByteTab];     // byte tables for H^1, H^2, H^4
+  uint8_t ntab[kNibTables][kNibTab];
+  uint8_t ltab[66][16];          // OCB: L_*, L_$, L_0..L_63
+};
+
+}  // namespace
+
+struct cmpi_ctx {
+  int alg = 0;
+  int device = 0;
+  int ncu = 256;
+  uint8_t key[16];
+  cmpi::dev::RoundKeys rk{};
+  cmpi::dev::RoundKeys drk{};
+  Blk H{};
+  DevTables* dt = nullptr;  // device
+  // per-G segment power tables, H^{kG}
+  mutable std::mutex mu;
+  mutable std::map<uint32_t, std::pair<u32x4*, uint32_t>> pw;
+  // internal scratch (partials, status) and staging for *_host
+  mutable void* scratch = nullptr;
+  mutable size_t scratch_cap = 0;
+  mutable uint8_t* stage = nullptr;
+  mutable size_t stage_cap = 0;
+  mutable hipStream_t hstream = nullptr;
+};
+
+namespace {
+
+int ensure_buf(void** p, size_t* cap, size_t need) {
+  if (need <= *cap) return CMPI_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  size_t sz = std::max(need, (size_t)1 << 20);
+  if (hipMalloc(p, sz) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc(%zu) failed", sz);
+  *cap = sz;
+  return CMPI_OK;
+}
+
+bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device).
+std::mutex g_attr_mu;
+std::map<std::pair<const void*, int>, int> g_attr_done;
+int set_lds_attr(const void* fn, int device, size_t lds) {
+  std::lock_guard<std::mutex> lk(g_attr_mu);
+  auto key = std::make_pair(fn, device);
+  auto it = g_attr_done.find(key);
+  if (it != g_attr_done.end() && it->second >= (int)lds) return CMPI_OK;
+  HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  g_attr_done[key] = (int)lds;
+  return CMPI_OK;
+}
+
+// ---------------------------------------------------------------- GCM launch planning
+struct GcmPlan {
+  int L;
+  uint32_t nb, nseg, G, r0;
+};
+
+// test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
+std::atomic<int> g_force_L{0};
+std::atomic<uint32_t> g_force_nseg{0};
+
+GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
+  GcmPlan p{};
+  p.nb = (uint32_t)((len + 15) / 16);
+  const uint64_t nx = (uint64_t)p.nb + 1;
+  const uint64_t target = (uint64_t)c->ncu * kGcmThreads;  // lanes that fill the chip once
+  p.L = 4;
+  if ((uint64_t)nrec * 1 >= target && nx >= 1) p.L = 1;
+  else if ((uint64_t)nrec * 2 >= target) p.L = 2;
+  if (nx < 8) p.L = 1;  // tiny records: one lane each
+  uint64_t nseg = 1;
+  const uint64_t lanes = (uint64_t)nrec * p.L;
+  if (lanes < target) {
+    const uint64_t want = (target + lanes - 1) / lanes;
+    const uint64_t maxseg = std::max<uint64_t>(1, nx / (uint64_t)(p.L * 32));  // >= 32 X-blocks per lane
+    nseg = std::min(want, maxseg);
+  }
+  if (g_force_L.load()) p.L = g_force_L.load();
+  if (g_force_nseg.load()) nseg = std::min<uint64_t>(g_force_nseg.load(), nx);
+  uint64_t G = (nx + nseg - 1) / nseg;
+  nseg = (nx + G - 1) / G;
+  p.G = (uint32_t)G;
+  p.nseg = (uint32_t)nseg;
+  p.r0 = (uint32_t)(nx - (nseg - 1) * G);
+  return p;
+}
+
+size_t gcm_ws_bytes(const GcmPlan& p, size_t nrec) {
+  if (p.nseg <= 1) return 0;
+  return (size_t)nrec * p.nseg * 16 + nrec * 16;
+}
+
+int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  auto it = c->pw.find(G);
+  if (it != c->pw.end() && it->second.second >= nseg) {
+    *out = it->second.first;
+    return CMPI_OK;
+  }
+  uint32_t n = std::max<uint32_t>(nseg, it != c->pw.end() ? it->second.second * 2 : 64);
+  std::vector<Blk> h(n);
+  const Blk HG = cmpi::gf_pow(c->H, G);
+  h[0] = cmpi::gf_one();
+  for (uint32_t k = 1; k < n; ++k) h[k] = cmpi::gf_mul(h[k - 1], HG);
+  u32x4* d = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)n * 16));
+  HIP_TRY(hipMemcpy(d, h.data(), (size_t)n * 16, hipMemcpyHostToDevice));
+  if (it != c->pw.end()) {
+    (void)hipFree(it->second.first);
+    it->second = {d, n};
+  } else {
+    c->pw[G] = {d, n};
+  }
+  *out = d;
+  return CMPI_OK;
+}
+
+template <int L, bool DEC>
+int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
+  auto fn = cmpi::dev::gcm_batch_kernel<L, DEC>;
+  int rc = set_lds_attr(reinterpret_cast<const void*>(fn), device, lds);
+  if (rc) return rc;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
+  HIP_TRY(hipGetLastError());
+  return CMPI_OK;
+}
+
+template <bool DEC>
+int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+              const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status,
+              void* workspace, void* stream) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (c->alg != CMPI_AES_128_GCM) return fail(CMPI_EINVAL, "ctx is not AES-128-GCM");
+  if (nrec == 0) return CMPI_OK;
+  if (!out || !in || !nonces) return fail(CMPI_EINVAL, "null buffer");
+  if (!aligned4(out) || !aligned4(in) || !aligned4(nonces) || (out_stride & 3) || (in_stride & 3) ||
+      (nonce_stride & 3))
+    return fail(CMPI_EINVAL, "pointers and strides must be 4-byte aligned");
+  if (len > 0xFFFFFFF0ull || nrec > 0x7FFFFFFFull) return fail(CMPI_EINVAL, "len/nrec out of range");
+  const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
+  if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
+    return fail(CMPI_EINVAL, "stride smaller than record");
+  DeviceGuard dg(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  const GcmPlan p = plan_gcm(c, len, nrec);
+  if ((uint64_t)nrec * p.nseg > 0xFFFFFFFFull) return fail(CMPI_EINVAL, "too many segments");
+
+  cmpi::dev::GcmArgs a{};
+  a.in = in;
+  a.out = out;
+  a.nonces = nonces;
+  a.in_stride = in_stride;
+  a.out_stride = out_stride;
+  a.nonce_stride = nonce_stride;
+  a.len = (uint32_t)len;
+  a.nb = p.nb;
+  a.nrec = (uint32_t)nrec;
+  a.nseg = p.nseg;
+  a.G = p.G;
+  a.r0 = p.r0;
+  a.ngroups = (uint32_t)(nrec * p.nseg);
+  a.tbase = (p.L > 1) ? 98304u : 65536u;
+  a.htab = reinterpret_cast<const u32x4*>(c->dt->htab[p.L == 1 ? 0 : (p.L == 2 ? 1 : 2)]);
+  a.ntab = reinterpret_cast<const u32x4*>(c->dt->ntab[0]);
+  a.te0 = c->dt->te0;
+  a.status = status;
+  a.rk = c->rk;
+  const u32x4* pw = nullptr;
+  if (p.nseg > 1) {
+    uint8_t* ws = (uint8_t*)workspace;
+    if (!ws) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      int rc = ensure_buf(&c->scratch, &c->scratch_cap, gcm_ws_bytes(p, nrec));
+      if (rc) return rc;
+      ws = (uint8_t*)c->scratch;
+    }
+    a.partial = reinterpret_cast<u32x4*>(ws);
+    a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
+    int rc = get_pw(c, p.G, p.nseg, &pw);
+    if (rc) return rc;
+  }
+  const size_t lds = (size_t)a.tbase + 32768;
+  const uint64_t want = ((uint64_t)a.ngroups * p.L + kGcmThreads - 1) / kGcmThreads;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->ncu));
+  int rc;
+  switch (p.L) {
+    case 1: rc = launch_gcm_main<1, DEC>(a, c->device, grid, lds, st); break;
+    case 2: rc = launch_gcm_main<2, DEC>(a, c->device, grid, lds, st); break;
+    default: rc = launch_gcm_main<4, DEC>(a, c->device, grid, lds, st); break;
+  }
+  if (rc) return rc;
+  if (p.nseg > 1) {
+    cmpi::dev::GcmCombineArgs ca{};
+    ca.in = in;
+    ca.out = out;
+    ca.in_stride = in_stride;
+    ca.out_stride = out_stride;
+    ca.len = (uint32_t)len;
+    ca.nb = p.nb;
+    ca.nrec = (uint32_t)nrec;
+    ca.nseg = p.nseg;
+    ca.partial = a.partial;
+    ca.ekj0 = a.ekj0;
+    ca.pw = pw;
+    ca.status = status;
+    hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(64), 0, st, ca);
+    HIP_TRY(hipGetLastError());
+  }
+  return CMPI_OK;
+}
+
+// ---------------------------------------------------------------- OCB
+struct OcbPlan {
+  uint32_t m, S, nchunks;
+};
+
+OcbPlan plan_ocb(const cmpi_ctx* c, size_t len, size_t nrec) {
+  OcbPlan p{};
+  p.m = (uint32_t)(len / 16);
+  const uint32_t ksteps = p.m / 64 + 1;
+  // aim for >= 8 waves per CU over the whole batch, >= 4 steps per chunk
+  const uint64_t target_waves = (uint64_t)c->ncu * 32;
+  uint64_t chunks = std::max<uint64_t>(1, (target_waves + nrec - 1) / std::max<size_t>(nrec, 1));
+  chunks = std::min<uint64_t>(chunks, std::max<uint32_t>(1, ksteps / 4));
+  p.S = (uint32_t)((ksteps + chunks - 1) / chunks);
+  p.nchunks = (ksteps + p.S - 1) / p.S;
+  return p;
+}
+
+template <bool DEC>
+int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+              const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status,
+              void* workspace, void* stream) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (c->alg != CMPI_AES_128_OCB) return fail(CMPI_EINVAL, "ctx is not AES-128-OCB");
+  if (nrec == 0) return CMPI_OK;
+  if (!out || !in || !nonces) return fail(CMPI_EINVAL, "null buffer");
+  if (!aligned4(out) || !aligned4(in) || !aligned4(nonces) || (out_stride & 3) || (in_stride & 3) ||
+      (nonce_stride & 3))
+    return fail(CMPI_EINVAL, "pointers and strides must be 4-byte aligned");
+  if (len > 0xFFFFFFF0ull || nrec > 0x7FFFFFFFull) return fail(CMPI_EINVAL, "len/nrec out of range");
+  const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
+  if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
+    return fail(CMPI_EINVAL, "stride smaller than record");
+  DeviceGuard dg(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  const OcbPlan p = plan_ocb(c, len, nrec);
+  const size_t part_bytes = (size_t)nrec * p.nchunks * 16;
+  const size_t off_bytes = (size_t)nrec * 16;
+  const size_t need = part_bytes + off_bytes + (size_t)nrec * 4;
+  uint8_t* ws = (uint8_t*)workspace;
+  if (!ws) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc = ensure_buf(&c->scratch, &c->scratch_cap, need);
+    if (rc) return rc;
+    ws = (uint8_t*)c->scratch;
+  }
+  u32x4* d_part = reinterpret_cast<u32x4*>(ws);
+  u32x4* d_off0 = reinterpret_cast<u32x4*>(ws + part_bytes);
+  int32_t* st_arr = status ? status : reinterpret_cast<int32_t*>(ws + part_bytes + off_bytes);
+
+  cmpi::dev::OcbOffsetArgs oa{};
+  oa.nonces = nonces;
+  oa.nonce_stride = nonce_stride;
+  oa.nrec = (uint32_t)nrec;
+  oa.te0 = c->dt->te0;
+  oa.off0 = d_off0;
+  oa.rk = c->rk;
+  hipLaunchKernelGGL(cmpi::dev::ocb_offset_kernel, dim3((uint32_t)((nrec + 255) / 256)), dim3(256), 32768, st, oa);
+  HIP_TRY(hipGetLastError());
+
+  cmpi::dev::OcbArgs a{};
+  a.in = in;
+  a.out = out;
+  a.nonces = nonces;
+  a.in_stride = in_stride;
+  a.out_stride = out_stride;
+  a.nonce_stride = nonce_stride;
+  a.len = (uint32_t)len;
+  a.m = p.m;
+  a.nrec = (uint32_t)nrec;
+  a.S = p.S;
+  a.nchunks = p.nchunks;
+  a.nitems = (uint32_t)(nrec * p.nchunks);
+  a.te0 = c->dt->te0;
+  a.td0 = c->dt->td0;
+  a.isb = c->dt->isb;
+  a.ltab = reinterpret_cast<const u32x4*>(c->dt->ltab);
+  a.off0 = d_off0;
+  a.partial = d_part;
+  a.rk = c->rk;
+  a.drk = c->drk;
+  const size_t lds = DEC ? cmpi::dev::kOcbLdsOpen : cmpi::dev::kOcbLdsSeal;
+  const uint32_t per_cu = DEC ? 2u : 4u;  // LDS-limited 512-thread blocks per CU
+  auto fn = cmpi::dev::ocb_batch_kernel<DEC>;
+  int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds);
+  if (rc) return rc;
+  const uint64_t waves = a.nitems;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + 7) / 8, (uint64_t)c->ncu * per_cu));
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(512), lds, st, a);
+  HIP_TRY(hipGetLastError());
+
+  cmpi::dev::OcbFinalArgs f{};
+  f.in = in;
+  f.out = out;
+  f.nonces = nonces;
+  f.in_stride = in_stride;
+  f.out_stride = out_stride;
+  f.nonce_stride = nonce_stride;
+  f.len = (uint32_t)len;
+  f.m = p.m;
+  f.nrec = (uint32_t)nrec;
+  f.nchunks = p.nchunks;
+  f.te0 = c->dt->te0;
+  f.ltab = a.ltab;
+  f.partial = d_part;
+  f.off0 = d_off0;
+  f.status = st_arr;
+  f.rk = c->rk;
+  hipLaunchKernelGGL(cmpi::dev::ocb_final_kernel<DEC>, dim3((uint32_t)((nrec + 255) / 256)), dim3(256),
+                     cmpi::dev::kOcbLdsSeal, st, f);
+  HIP_TRY(hipGetLastError());
+  if (DEC) {
+    hipLaunchKernelGGL(cmpi::dev::zero_failed_kernel, dim3((uint32_t)nrec), dim3(256), 0, st, out,
+                       (uint64_t)out_stride, (uint32_t)len, (const int32_t*)st_arr);
+    HIP_TRY(hipGetLastError());
+  }
+  return CMPI_OK;
+}
+
+// ---------------------------------------------------------------- host staging
+template <bool DEC, bool OCB>
+int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+              const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (nrec == 0) return CMPI_OK;
+  if (!out || !in || !nonces) return fail(CMPI_EINVAL, "null buffer");
+  const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
+  if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
+    return fail(CMPI_EINVAL, "stride smaller than record");
+  DeviceGuard dg(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);  // staging buffers are per ctx
+  if (!c->hstream) HIP_TRY(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
+  auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t ip = up16(in_rec), op = up16(out_rec);
+  const size_t in_b = ip * nrec, out_b = op * nrec, n_b = 16 * nrec, st_b = up16(4 * nrec);
+  int rc = ensure_buf((void**)&c->stage, &c->stage_cap, in_b + out_b + n_b + st_b);
+  if (rc) return rc;
+  uint8_t* d_in = c->stage;
+  uint8_t* d_out = d_in + in_b;
+  uint8_t* d_n = d_out + out_b;
+  int32_t* d_st = reinterpret_cast<int32_t*>(d_n + n_b);
+  hipStream_t s = c->hstream;
+  if (in_rec) HIP_TRY(hipMemcpy2DAsync(d_in, ip, in, nrec > 1 ? in_stride : in_rec, in_rec, nrec, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(d_n, 16, nonces, nrec > 1 ? nonce_stride : 12, 12, nrec, hipMemcpyHostToDevice, s));
+  c->mu.unlock();  // the batch call takes the lock itself for its scratch
+  if (OCB)
+    rc = ocb_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nrec, DEC ? d_st : nullptr, nullptr, s);
+  else
+    rc = gcm_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nrec, DEC ? d_st : nullptr, nullptr, s);
+  c->mu.lock();
+  if (rc) return rc;
+  if (out_rec) HIP_TRY(hipMemcpy2DAsync(out, nrec > 1 ? out_stride : out_rec, d_out, op, out_rec, nrec, hipMemcpyDeviceToHost, s));
+  std::vector<int32_t> hst;
+  if (DEC) {
+    hst.resize(nrec);
+    HIP_TRY(hipMemcpyAsync(hst.data(), d_st, 4 * nrec, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  if (DEC) {
+    size_t bad = 0;
+    for (size_t i = 0; i < nrec; ++i) bad += hst[i] == 0;
+    if (status) memcpy(status, hst.data(), 4 * nrec);
+    if (bad) return fail(CMPI_EAUTH, "%zu of %zu records failed authentication", bad, nrec);
+  }
+  return CMPI_OK;
+}
+
+}  // namespace
+
+// ================================================================= exported C ABI
+extern "C" {
+
+const char* cmpi_version(void) { return "cmpi_aead 0.1 (gfx950)"; }
+const char* cmpi_last_error(void) { return g_err.c_str(); }
+
+int cmpi_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_len, int device) {
+  if (!key || key_len != 16) {
+    fail(CMPI_EINVAL, "key_len must be 16 (AES-128)");
+    return nullptr;
+  }
+  if (!(tag_len == 0 || tag_len == 16)) {
+    fail(CMPI_EINVAL, "tag_len must be 0 or 16");
+    return nullptr;
+  }
+  if (alg < CMPI_AES_128_GCM || alg > CMPI_AES_128_ECB) {
+    fail(CMPI_EINVAL, "unknown algorithm %d", alg);
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    fail(CMPI_ENODEV, "no HIP device %d (count %d)", device, ndev);
+    return nullptr;
+  }
+  DeviceGuard dg(device);
+  auto* c = new cmpi_ctx();
+  c->alg = alg;
+  c->device = device;
+  memcpy(c->key, key, 16);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->ncu = prop.multiProcessorCount;
+  cmpi::aes128_expand_words(key, c->rk.w);
+  cmpi::aes128_dec_words(c->rk.w, c->drk.w);
+  uint32_t z[4] = {0, 0, 0, 0}, h[4];
+  cmpi::aes128_encrypt_words_host(c->rk.w, z, h);  // H = E_K(0^128), L_* for OCB
+  memcpy(c->H.b, h, 16);
+
+  auto* ht = new DevTables();
+  memcpy(ht->te0, cmpi::kAes.te0, sizeof ht->te0);
+  memcpy(ht->td0, cmpi::kAes.td0, sizeof ht->td0);
+  for (int x = 0; x < 256; ++x) ht->isb[x] = cmpi::kAes.inv_sbox[x];
+  if (alg == CMPI_AES_128_GCM) {
+    const Blk H2 = cmpi::gf_mul(c->H, c->H), H3 = cmpi::gf_mul(H2, c->H), H4 = cmpi::gf_mul(H2, H2);
+    cmpi::build_byte_table(c->H, reinterpret_cast<Blk*>(ht->htab[0]));
+    cmpi::build_byte_table(H2, reinterpret_cast<Blk*>(ht->htab[1]));
+    cmpi::build_byte_table(H4, reinterpret_cast<Blk*>(ht->htab[2]));
+    const Blk pw[4] = {c->H, H2, H3, H4};
+    for (int i = 0; i < 4; ++i) cmpi::build_nibble_table(pw[i], reinterpret_cast<Blk*>(ht->ntab[i]));
+  }
+  if (alg == CMPI_AES_128_OCB) {
+    // RFC 7253 §4.1: L_* = E_K(0), L_$ = double(L_*), L_0 = double(L_$), L_i = double(L_{i-1})
+    auto dbl = [](const uint8_t* in, uint8_t* o) {
+      const uint8_t carry = in[0] >> 7;
+      for (int i = 0; i < 15; ++i) o[i] = (uint8_t)((in[i] << 1) | (in[i + 1] >> 7));
+      o[15] = (uint8_t)((in[15] << 1) ^ (carry ? 0x87 : 0));
+    };
+    memcpy(ht->ltab[0], c->H.b, 16);
+    for (int i = 1; i < 66; ++i) dbl(ht->ltab[i - 1], ht->ltab[i]);
+  }
+  if (hipMalloc(&c->dt, sizeof(DevTables)) != hipSuccess) {
+    fail(CMPI_ENOMEM, "hipMalloc tables failed");
+    delete ht;
+    delete c;
+    return nullptr;
+  }
+  hipError_t e = hipMemcpy(c->dt, ht, sizeof(DevTables), hipMemcpyHostToDevice);
+  delete ht;
+  if (e != hipSuccess) {
+    fail(CMPI_EHIP, "hipMemcpy tables: %s", hipGetErrorString(e));
+    (void)hipFree(c->dt);
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+void cmpi_ctx_free(cmpi_ctx* c) {
+  if (!c) return;
+  DeviceGuard dg(c->device);
+  for (auto& kv : c->pw) (void)hipFree(kv.second.first);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->stage) (void)hipFree(c->stage);
+  if (c->hstream) (void)hipStreamDestroy(c->hstream);
+  if (c->dt) (void)hipFree(c->dt);
+  memset(c->key, 0, 16);
+  delete c;
+}
+
+int cmpi_ctx_device(const cmpi_ctx* c) { return c ? c->device : -1; }
+
+void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
+  g_force_L.store(lanes_per_record == 1 || lanes_per_record == 2 || lanes_per_record == 4 ? lanes_per_record : 0);
+  g_force_nseg.store(segments);
+}
+
+int cmpi_debug_gcm_plan(const cmpi_ctx* c, size_t len, size_t nrec, uint32_t out[4]) {
+  if (!c || !out) return fail(CMPI_EINVAL, "null argument");
+  const GcmPlan p = plan_gcm(c, len, nrec);
+  out[0] = (uint32_t)p.L;
+  out[1] = p.nseg;
+  out[2] = p.G;
+  out[3] = p.r0;
+  return CMPI_OK;
+}
+
+size_t cmpi_gcm_workspace_size(const cmpi_ctx* c, size_t len, size_t nrec) {
+  if (!c) return 0;
+  return gcm_ws_bytes(plan_gcm(c, len, nrec), nrec);
+}
+
+int cmpi_gcm_seal_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                        const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, void* workspace,
+                        void* stream) {
+  return gcm_batch<false>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, nullptr, workspace,
+                          stream);
+}
+
+int cmpi_gcm_open_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                        const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status,
+                        void* workspace, void* stream) {
+  return gcm_batch<true>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, status, workspace,
+                         stream);
+}
+
+int cmpi_gcm_seal_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                       const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec) {
+  return aead_host<false, false>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, nullptr);
+}
+
+int cmpi_gcm_open_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                       const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status) {
+  return aead_host<true, false>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, status);
+}
+
+size_t cmpi_ocb_workspace_size(const cmpi_ctx* c, size_t len, size_t nrec) {
+  if (!c) return 0;
+  const OcbPlan p = plan_ocb(c, len, nrec);
+  return (size_t)nrec * p.nchunks * 16 + nrec * 16 + nrec * 4;
+}
+
+int cmpi_ocb_seal_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                        const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, void* workspace,
+                        void* stream) {
+  return ocb_batch<false>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, nullptr, workspace,
+                          stream);
+}
+
+int cmpi_ocb_open_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                        const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status,
+                        void* workspace, void* stream) {
+  return ocb_batch<true>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, status, workspace,
+                         stream);
+}
+
+static int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, const uint8_t ctr[16],
+                      void* stream) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (c->alg != CMPI_AES_128_CTR && c->alg != CMPI_AES_128_GCM && c->alg != CMPI_AES_128_ECB)
+    return fail(CMPI_EINVAL, "ctx algorithm cannot run CTR");
+  if (!ctr || !out) return fail(CMPI_EINVAL, "null argument");
+  if (n == 0) return CMPI_OK;
+  if (!aligned4(out) || (in && !aligned4(in))) return fail(CMPI_EINVAL, "pointers must be 4-byte aligned");
+  DeviceGuard dg(c->device);
+  cmpi::dev::CtrArgs a{};
+  a.in = in;
+  a.out = out;
+  a.n = n;
+  a.nblk = (n + 15) / 16;
+  a.ctr_hi = cmpi::be64(ctr);
+  a.ctr_lo = cmpi::be64(ctr + 8);
+  a.te0 = c->dt->te0;
+  a.rk = c->rk;
+  const uint64_t blocks = (a.nblk + 511) / 512;  // 2 blocks per thread per pass
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 4));
+  hipStream_t st = (hipStream_t)stream;
+  if (in) hipLaunchKernelGGL(cmpi::dev::ctr_kernel<true>, dim3(grid), dim3(256), 32768, st, a);
+  else hipLaunchKernelGGL(cmpi::dev::ctr_kernel<false>, dim3(grid), dim3(256), 32768, st, a);
+  HIP_TRY(hipGetLastError());
+  return CMPI_OK;
+}
+
+int cmpi_ctr_xor(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, const uint8_t ctr_block[16],
+                 void* stream) {
+  if (!in) return fail(CMPI_EINVAL, "null input");
+  return ctr_launch(c, out, in, n, ctr_block, stream);
+}
+
+int cmpi_ctr_keystream(const cmpi_ctx* c, uint8_t* out, size_t nblocks, const uint8_t ctr_block[16], void* stream) {
+  return ctr_launch(c, out, nullptr, nblocks * 16, ctr_block, stream);
+}
+
+void cmpi_iv_count(uint8_t iv[16], unsigned long cter) {
+  uint32_t n = 16, c = (uint32_t)cter;  // uint32 accumulator exactly as send.c:1021-1029
+  do {
+    --n;
+    c += iv[n];
+    iv[n] = (uint8_t)c;
+    c >>= 8;
+  } while (n);
+}
+
+void cmpi_iv_count_out(uint8_t iv[16], unsigned long cter, const uint8_t in[16]) {
+  uint32_t n = 16, c = (uint32_t)cter;  // send.c:1032-1041
+  do {
+    --n;
+    c += in[n];
+    iv[n] = (uint8_t)c;
+    c >>= 8;
+  } while (n);
+}
+
+int cmpi_ecb_encrypt(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t nblocks, void* stream) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (!out || !in) return fail(CMPI_EINVAL, "null buffer");
+  if (nblocks == 0) return CMPI_OK;
+  if (!aligned4(out) || !aligned4(in)) return fail(CMPI_EINVAL, "pointers must be 4-byte aligned");
+  DeviceGuard dg(c->device);
+  cmpi::dev::EcbArgs a{};
+  a.in = in;
+  a.out = out;
+  a.nblk = nblocks;
+  a.te0 = c->dt->te0;
+  a.rk = c->rk;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 255) / 256, (uint64_t)c->ncu * 4));
+  hipLaunchKernelGGL(cmpi::dev::ecb_kernel, dim3(grid), dim3(256), 32768, (hipStream_t)stream, a);
+  HIP_TRY(hipGetLastError());
+  return CMPI_OK;
+}
+
+cmpi_ctx* cmpi_ctx_new_subkey(const cmpi_ctx* base, const uint8_t v[16]) {
+  if (!base || !v) {
+    fail(CMPI_EINVAL, "null argument");
+    return nullptr;
+  }
+  uint8_t kp[16];
+  {
+    DeviceGuard dg(base->device);
+    uint8_t* d = nullptr;
+    if (hipMalloc(&d, 32) != hipSuccess) {
+      fail(CMPI_ENOMEM, "hipMalloc failed");
+      return nullptr;
+    }
+    int rc = CMPI_OK;
+    if (hipMemcpy(d, v, 16, hipMemcpyHostToDevice) != hipSuccess) rc = fail(CMPI_EHIP, "H2D V failed");
+    if (!rc) rc = cmpi_ecb_encrypt(base, d + 16, d, 1, nullptr);
+    if (!rc && hipMemcpy(kp, d + 16, 16, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(CMPI_EHIP, "D2H K' failed");
+    (void)hipFree(d);
+    if (rc) return nullptr;
+  }
+  cmpi_ctx* c = cmpi_ctx_new(CMPI_AES_128_GCM, kp, 16, 0, base->device);
+  memset(kp, 0, 16);
+  return c;
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+// ctr_kernels.hpp — AES-128-CTR keystream (+XOR) and AES-128-ECB over device buffers (gfx950).
+//
+// CTR: block j uses counter (ctr_hi:ctr_lo) + j as a 128-bit big-endian integer — the
+// EVP_aes_128_ctr increment behind EVP_EncryptUpdate in CryptMPI's 700/702 paths
+// (MV/src/mpi/pt2pt/send.c:985-1008, :1716-1727, :1805-1808; recv.c:869-937, :1187-1220).
+// The keystream-only variant is generateCommonEncMask's E_K(IV_A + c) over zeros
+// (send.c:1162-1266).  ECB: EVP_EncryptUpdate(ctx_enc, …) for the 602 sub-key (send.c:583).
+// Each thread owns two 16-byte blocks per iteration (ILP for the LDS pipe), consecutive lanes
+// own consecutive blocks (1 KiB coalesced per wave-instruction).
+#pragma once
+#include "aes_device.hpp"
+
+namespace cmpi {
+namespace dev {
+
+struct CtrArgs {
+  const uint8_t* in;  // null for keystream-only
+  uint8_t* out;
+  uint64_t n;         // bytes (keystream: nblocks*16)
+  uint64_t nblk;      // ceil(n/16)
+  uint64_t ctr_hi, ctr_lo;  // counter block as two big-endian halves
+  const uint32_t* te0;
+  RoundKeys rk;
+};
+
+__device__ __forceinline__ void ctr_words(uint64_t hi, uint64_t lo, uint64_t j, uint32_t& w0, uint32_t& w1,
+                                          uint32_t& w2, uint32_t& w3) {
+  const uint64_t l2 = lo + j;
+  const uint64_t h2 = hi + (l2 < lo ? 1u : 0u);
+  w0 = __builtin_bswap32((uint32_t)(h2 >> 32));
+  w1 = __builtin_bswap32((uint32_t)h2);
+  w2 = __builtin_bswap32((uint32_t)(l2 >> 32));
+  w3 = __builtin_bswap32((uint32_t)l2);
+}
+
+template <bool XOR_IN>
+__device__ __forceinline__ void ctr_emit(const CtrArgs& a, uint64_t j, u32x4 ks) {
+  const uint64_t off = j * 16u;
+  if (!XOR_IN) {
+    *reinterpret_cast<u32x4a*>(a.out + off) = ks;
+    return;
+  }
+  if (off + 16u <= a.n) {
+    const u32x4 v = *reinterpret_cast<const u32x4a*>(a.in + off);
+    *reinterpret_cast<u32x4a*>(a.out + off) = v ^ ks;
+  } else {
+    const uint32_t rem = (uint32_t)(a.n - off);
+    store_partial(a.out + off, load_partial(a.in + off, rem) ^ ks, rem);
+  }
+}
+
+template <bool XOR_IN>
+__global__ __launch_bounds__(256) void ctr_kernel(CtrArgs a) {
+  stage_te0(a.te0, 0u);
+  __syncthreads();
+  const uint32_t lb = (threadIdx.x & 31u) << 2;
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; j + nthreads < a.nblk; j += 2u * nthreads) {
+    const uint64_t jb = j + nthreads;
+    uint32_t s0, s1, s2, s3, t0, t1, t2, t3;
+    ctr_words(a.ctr_hi, a.ctr_lo, j, s0, s1, s2, s3);
+    ctr_words(a.ctr_hi, a.ctr_lo, jb, t0, t1, t2, t3);
+    aes128_enc2(a.rk, lb, s0, s1, s2, s3, t0, t1, t2, t3);
+    ctr_emit<XOR_IN>(a, j, u32x4{s0, s1, s2, s3});
+    ctr_emit<XOR_IN>(a, jb, u32x4{t0, t1, t2, t3});
+  }
+  if (j < a.nblk) {
+    uint32_t s0, s1, s2, s3;
+    ctr_words(a.ctr_hi, a.ctr_lo, j, s0, s1, s2, s3);
+    aes128_enc(a.rk, lb, s0, s1, s2, s3);
+    ctr_emit<XOR_IN>(a, j, u32x4{s0, s1, s2, s3});
+  }
+}
+
+struct EcbArgs {
+  const uint8_t* in;
+  uint8_t* out;
+  uint64_t nblk;
+  const uint32_t* te0;
+  RoundKeys rk;
+};
+
+__global__ __launch_bounds__(256) void ecb_kernel(EcbArgs a) {
+  stage_te0(a.te0, 0u);
+  __syncthreads();
+  const uint32_t lb = (threadIdx.x & 31u) << 2;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.nblk; j += (uint64_t)gridDim.x * blockDim.x) {
+    const u32x4 v = *reinterpret_cast<const u32x4a*>(a.in + 16u * j);
+    uint32_t s0 = v[0], s1 = v[1], s2 = v[2], s3 = v[3];
+    aes128_enc(a.rk, lb, s0, s1, s2, s3);
+    *reinterpret_cast<u32x4a*>(a.out + 16u * j) = u32x4{s0, s1, s2, s3};
+  }
+}
+
+}  // namespace dev
+}  // namespace cmpi

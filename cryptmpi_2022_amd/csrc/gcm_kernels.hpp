@@ -1,0 +1,218 @@
+// gcm_kernels.hpp — AES-128-GCM batched seal/open for uniform record batches (gfx950).
+//
+// Work decomposition (DESIGN.md §"GCM kernel"):
+//   record r (len bytes, nb = ceil(len/16) data blocks) has the GHASH input sequence
+//   X_0..X_nb-1 = ciphertext blocks, X_nb = length block.  That sequence is cut into nseg
+//   segments from the END (every segment but the first has exactly G X-blocks), and every
+//   (record, segment) is one "group" of L lanes (L in {1,2,4}) inside one wavefront.  Lane q of
+//   a group owns segment slots u = q, q+L, q+2L, ...: it runs AES-CTR on those data blocks,
+//   writes ct/pt, and folds its X-blocks into a private Horner accumulator with multiplier H^L
+//   (byte table in LDS).  The L partial sums are then weighted by H^w (w = slots after the
+//   lane's last one, nibble tables in LDS), XOR-reduced with wavefront shuffles, and the tag is
+//   finished in-kernel when the record is one segment; otherwise partials go to HBM and
+//   gcm_combine_kernel multiplies them by H^{k·G} and finishes the tag.  Segment 0 also owns the
+//   extra slot that computes E_K(J0).
+// The arithmetic it implements is BoringSSL's aead_aes_gcm seal/open behind
+// EVP_AEAD_CTX_seal/open (aead.h:256-285) — SP 800-38D with a 96-bit IV, no AAD.
+#pragma once
+#include "aes_device.hpp"
+
+namespace cmpi {
+namespace dev {
+
+struct GcmArgs {
+  const uint8_t* in;
+  uint8_t* out;
+  const uint8_t* nonces;
+  uint64_t in_stride, out_stride, nonce_stride;
+  uint32_t len;     // plaintext bytes per record
+  uint32_t nb;      // data blocks per record
+  uint32_t nrec;
+  uint32_t nseg;    // segments per record
+  uint32_t G;       // X-blocks per segment (all but the first)
+  uint32_t r0;      // X-blocks in the first segment
+  uint32_t ngroups; // nrec * nseg
+  uint32_t tbase;   // LDS offset of the replicated Te0
+  const u32x4* htab;   // byte table of H^L (global), 4096 entries
+  const u32x4* ntab;   // nibble tables of H^1..H^L (global), L*512 entries (L > 1)
+  const uint32_t* te0; // Te0 (global), 256 words
+  u32x4* partial;      // nrec*nseg segment partials (nseg > 1)
+  u32x4* ekj0;         // nrec E_K(J0) (nseg > 1)
+  int32_t* status;     // open: per-record result (may be null)
+  RoundKeys rk;
+};
+
+__device__ __forceinline__ u32x4 ld_blk(const uint8_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
+__device__ __forceinline__ void st_blk(uint8_t* p, u32x4 v) { *reinterpret_cast<u32x4a*>(p) = v; }
+
+template <int L, bool DECRYPT>
+__global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
+  // ---- stage tables: GHASH byte table @0, nibble tables @64K, Te0 x32 @tbase
+  stage_copy(a.htab, 0u, 4096u);
+  if (L > 1) stage_copy(a.ntab, 65536u, (uint32_t)L * 512u);
+  stage_te0(a.te0, a.tbase);
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lb = a.tbase | ((lane & 31u) << 2);
+  const uint32_t q = threadIdx.x & (uint32_t)(L - 1);
+  const uint32_t nb = a.nb;
+  const uint32_t rem = a.len - 16u * (nb ? nb - 1u : 0u);  // bytes in the last data block (1..16)
+  // length block [len(A)]_64 || [len(C)]_64 in memory order
+  const uint64_t cbits = (uint64_t)a.len * 8u;
+  const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
+
+  const uint32_t groups_per_iter = (gridDim.x * blockDim.x) / (uint32_t)L;
+  for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / (uint32_t)L; g < a.ngroups; g += groups_per_iter) {
+    const uint32_t r = (a.nseg == 1) ? g : g / a.nseg;
+    const uint32_t s = g - r * a.nseg;
+    const uint32_t x0 = (s == 0) ? 0u : a.r0 + (s - 1u) * a.G;
+    const uint32_t x1 = a.r0 + s * a.G;
+    const uint32_t nxs = x1 - x0;                   // X-blocks in this segment
+    const uint32_t nslots = nxs + (s == 0 ? 1u : 0u);  // + the J0 slot
+    const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
+    uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
+    const uint32_t* np = reinterpret_cast<const uint32_t*>(a.nonces + (uint64_t)r * a.nonce_stride);
+    const uint32_t n0 = np[0], n1 = np[1], n2 = np[2];
+
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    u32x4 ekj0 = {0u, 0u, 0u, 0u};
+
+    // process slot u's AES output `ks`; returns the X block (or J0 handled)
+    auto consume = [&](uint32_t u, u32x4 ks) {
+      if (u >= nxs) {  // J0 slot
+        ekj0 = ks;
+        return;
+      }
+      const uint32_t j = x0 + u;
+      u32x4 x;
+      if (j < nb) {
+        const uint8_t* ip = in_rec + 16u * j;
+        uint8_t* op = out_rec + 16u * j;
+        if (j + 1u < nb || rem == 16u) {
+          const u32x4 v = ld_blk(ip);
+          const u32x4 o = v ^ ks;
+          st_blk(op, o);
+          x = DECRYPT ? v : o;
+        } else {
+          const u32x4 v = load_partial(ip, rem);
+          const u32x4 o = mask_bytes(v ^ ks, rem);
+          store_partial(op, o, rem);
+          x = DECRYPT ? v : o;
+        }
+      } else {
+        x = lenblk;
+      }
+      acc = gmul_byte(acc) ^ x;
+    };
+
+    for (uint32_t u = q; u < nslots; u += (uint32_t)L) {
+      const uint32_t c = (u >= nxs) ? 1u : 2u + x0 + u;
+      uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = __builtin_bswap32(c);
+      aes128_enc(a.rk, lb, s0, s1, s2, s3);
+      consume(u, u32x4{s0, s1, s2, s3});
+    }
+
+    // ---- weight the lane's Horner sum by H^w, w = nxs - (lane's last X slot)
+    u32x4 f;
+    if (L == 1) {
+      f = gmul_byte(acc);  // L = 1: byte table holds H, w = 1
+    } else {
+      f = u32x4{0u, 0u, 0u, 0u};
+      if (q < nxs) {
+        const uint32_t ulast = q + (uint32_t)L * ((nxs - 1u - q) / (uint32_t)L);
+        const uint32_t w = nxs - ulast;  // 1..L
+        f = gmul_nib(acc, 65536u + (w - 1u) * 8192u);
+      }
+    }
+    if (a.nseg == 1) f ^= ekj0;
+#pragma unroll
+    for (int m = 1; m < L; m <<= 1) f ^= shfl_xor4(f, m);
+
+    if (a.nseg > 1) {
+      if (q == 0) a.partial[g] = f;
+      if (s == 0 && (nxs % (uint32_t)L) == q) a.ekj0[r] = ekj0;  // lane that owned slot nxs
+      continue;
+    }
+    // single-segment record: finish the tag here
+    if (!DECRYPT) {
+      if (q == 0) {
+        uint8_t* tp = out_rec + a.len;
+        if ((a.len & 3u) == 0u) st_blk(tp, f);
+        else store_partial(tp, f, 16u);
+      }
+    } else {
+      int ok = 1;
+      if (q == 0) {
+        const uint8_t* tp = in_rec + a.len;
+        const u32x4 t = ((a.len & 3u) == 0u) ? ld_blk(tp) : load_partial(tp, 16u);
+        const u32x4 d = t ^ f;
+        ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+        if (a.status) a.status[r] = ok;
+      }
+      if (L > 1) ok = __shfl(ok, (int)(lane & ~(uint32_t)(L - 1)));
+      if (!ok) {  // zero-fill this record's plaintext (aead.h:276-278)
+        for (uint32_t v = q; v < nxs; v += (uint32_t)L) {
+          const uint32_t j = x0 + v;
+          if (j >= nb) continue;
+          uint8_t* op = out_rec + 16u * j;
+          if (j + 1u < nb || rem == 16u) st_blk(op, u32x4{0u, 0u, 0u, 0u});
+          else store_partial(op, u32x4{0u, 0u, 0u, 0u}, rem);
+        }
+      }
+    }
+  }
+}
+
+struct GcmCombineArgs {
+  const uint8_t* in;   // open: ct||tag records (for the received tag)
+  uint8_t* out;        // seal: ct||tag records (tag written); open: pt records (zeroed on failure)
+  uint64_t in_stride, out_stride;
+  uint32_t len, nb, nrec, nseg;
+  const u32x4* partial;  // nrec*nseg
+  const u32x4* ekj0;     // nrec
+  const u32x4* pw;       // pw[k] = H^{k*G}, k < nseg
+  int32_t* status;
+};
+
+// One 64-lane block per record: Y = XOR_s partial[s] · H^{(nseg-1-s)·G}; tag = Y ^ E_K(J0).
+template <bool DECRYPT>
+__global__ __launch_bounds__(64) void gcm_combine_kernel(GcmCombineArgs a) {
+  const uint32_t r = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  u32x4 y = {0u, 0u, 0u, 0u};
+  for (uint32_t s = lane; s < a.nseg; s += 64u) {
+    const u32x4 p = a.partial[(uint64_t)r * a.nseg + s];
+    const uint32_t k = a.nseg - 1u - s;
+    y ^= (k == 0u) ? p : gmul_generic(p, a.pw[k]);
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) y ^= shfl_xor4(y, m);
+  y ^= a.ekj0[r];
+  int ok = 1;
+  if (!DECRYPT) {
+    if (lane == 0) {
+      uint8_t* tp = a.out + (uint64_t)r * a.out_stride + a.len;
+      if ((a.len & 3u) == 0u) st_blk(tp, y);
+      else store_partial(tp, y, 16u);
+    }
+    return;
+  }
+  if (lane == 0) {
+    const uint8_t* tp = a.in + (uint64_t)r * a.in_stride + a.len;
+    const u32x4 t = ((a.len & 3u) == 0u) ? ld_blk(tp) : load_partial(tp, 16u);
+    const u32x4 d = t ^ y;
+    ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+    if (a.status) a.status[r] = ok;
+  }
+  ok = __shfl(ok, 0);
+  if (!ok) {
+    uint8_t* o = a.out + (uint64_t)r * a.out_stride;
+    const uint32_t full = a.len & ~3u;
+    for (uint32_t i = lane * 4u; i < full; i += 64u * 4u) *reinterpret_cast<uint32_t*>(o + i) = 0u;
+    for (uint32_t i = full + lane; i < a.len; i += 64u) o[i] = 0u;
+  }
+}
+
+}  // namespace dev
+}  // namespace cmpi

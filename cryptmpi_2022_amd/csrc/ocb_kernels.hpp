@@ -1,0 +1,221 @@
+// ocb_kernels.hpp — AES-128-OCB3 (RFC 7253, TAGLEN 128, 96-bit nonce, no AAD) batched
+// seal/open for uniform record batches (gfx950).  The reference advertises OCB
+// (MV2_SECURITY_APPROACH=402, README.md:128-129) but ships none (OPENSSL_NO_OCB); this follows
+// RFC 7253 and is pinned against its Appendix A and OpenSSL 3.
+//
+// Offsets in closed form: Offset_i = Offset_0 ^ XOR{ L_k : bit k of gray(i) }, gray(i) = i^(i>>1).
+// A wavefront owns a "chunk" of S consecutive 64-block steps of one record; at step k lane l
+// handles RFC block index i = 64k + l, so loads are 1 KiB coalesced, and
+//   gray(64k + l) = ((k<<6) ^ (k<<5)) ^ gray(l)
+// splits the offset into a lane constant D_l = XOR L over gray(l) and a wave-uniform U_k with
+// U_{k+1} = U_k ^ L_5 ^ L_{6+ntz(k+1)}: two XORs of broadcast LDS values per step.
+// The checksum (XOR of plaintext blocks) is reduced per wave with shuffles, written per chunk,
+// and ocb_final_kernel XORs the chunk partials, handles the trailing partial block and
+// computes Tag = E_K(Checksum ^ Offset ^ L_$).
+#pragma once
+#include "aes_device.hpp"
+
+namespace cmpi {
+namespace dev {
+
+struct OcbArgs {
+  const uint8_t* in;
+  uint8_t* out;
+  const uint8_t* nonces;
+  uint64_t in_stride, out_stride, nonce_stride;
+  uint32_t len, m;        // bytes, full blocks per record
+  uint32_t nrec, S;       // records, 64-block steps per chunk
+  uint32_t nchunks;       // chunks per record
+  uint32_t nitems;        // nrec * nchunks
+  const uint32_t* te0;
+  const uint32_t* td0;
+  const uint32_t* isb;    // inverse S-box as words
+  const u32x4* ltab;      // [0] = L_*, [1] = L_$, [2 + i] = L_i (i < 64)
+  const u32x4* off0;      // per-record Offset_0 (ocb_offset_kernel)
+  u32x4* partial;         // nitems checksum partials
+  RoundKeys rk;           // encryption keys
+  RoundKeys drk;          // equivalent-inverse-cipher keys
+};
+
+// LDS layouts.  seal: Te0 x32 @0, L table @32K (33 KiB).  open: Td0 x32 @0, Si x32 @32K,
+// L table @64K (65 KiB).  offset / final kernels: Te0 @0, L @32K.
+constexpr uint32_t kOcbLSeal = 32768u;
+constexpr uint32_t kOcbLOpen = 65536u;
+constexpr uint32_t kOcbLdsSeal = kOcbLSeal + 66u * 16u;
+constexpr uint32_t kOcbLdsOpen = kOcbLOpen + 66u * 16u;
+
+__device__ __forceinline__ u32x4 ocb_l(uint32_t base, uint32_t idx) { return lds128(base + idx * 16u); }
+
+// Offset_0 from the 96-bit nonce (RFC 7253 §4.2): Nonce block = 0^31 || 1 || N.
+__device__ __forceinline__ u32x4 ocb_offset0(const RoundKeys& rk, uint32_t lb, uint32_t n0, uint32_t n1,
+                                             uint32_t n2) {
+  const uint32_t bottom = (n2 >> 24) & 0x3fu;
+  uint32_t s0 = 0x01000000u, s1 = n0, s2 = n1, s3 = n2 & 0xc0ffffffu;
+  aes128_enc(rk, lb, s0, s1, s2, s3);  // Ktop
+  const uint64_t k0 = ((uint64_t)__builtin_bswap32(s0) << 32) | __builtin_bswap32(s1);
+  const uint64_t k1 = ((uint64_t)__builtin_bswap32(s2) << 32) | __builtin_bswap32(s3);
+  const uint64_t k2 = k0 ^ ((k0 << 8) | (k1 >> 56));  // Stretch bits 128..191
+  uint64_t o0 = k0, o1 = k1;
+  if (bottom) {
+    o0 = (k0 << bottom) | (k1 >> (64u - bottom));
+    o1 = (k1 << bottom) | (k2 >> (64u - bottom));
+  }
+  return u32x4{__builtin_bswap32((uint32_t)(o0 >> 32)), __builtin_bswap32((uint32_t)o0),
+               __builtin_bswap32((uint32_t)(o1 >> 32)), __builtin_bswap32((uint32_t)o1)};
+}
+
+__device__ __forceinline__ u32x4 ocb_lsum(uint32_t base, uint64_t bits) {  // XOR of L_k over set bits
+  u32x4 r = {0u, 0u, 0u, 0u};
+  while (bits) {
+    const uint32_t k = (uint32_t)__builtin_ctzll(bits);
+    r ^= ocb_l(base, 2u + k);
+    bits &= bits - 1u;
+  }
+  return r;
+}
+
+// Offset_0 per record (one thread per record).
+struct OcbOffsetArgs {
+  const uint8_t* nonces;
+  uint64_t nonce_stride;
+  uint32_t nrec;
+  const uint32_t* te0;
+  u32x4* off0;
+  RoundKeys rk;
+};
+
+__global__ __launch_bounds__(256) void ocb_offset_kernel(OcbOffsetArgs a) {
+  stage_te0(a.te0, 0u);
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.nrec) return;
+  const uint32_t* np = reinterpret_cast<const uint32_t*>(a.nonces + (uint64_t)r * a.nonce_stride);
+  a.off0[r] = ocb_offset0(a.rk, (threadIdx.x & 31u) << 2, np[0], np[1], np[2]);
+}
+
+template <bool DECRYPT>
+__global__ __launch_bounds__(512) void ocb_batch_kernel(OcbArgs a) {
+  constexpr uint32_t LB = DECRYPT ? kOcbLOpen : kOcbLSeal;
+  if (DECRYPT) {
+    stage_rep32(a.td0, 0u);
+    stage_rep32(a.isb, 32768u);
+  } else {
+    stage_te0(a.te0, 0u);
+  }
+  stage_copy(a.ltab, LB, 66u);
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t l32 = (lane & 31u) << 2;
+  const uint32_t lbe = l32, lbd = l32, lbs = 32768u | l32;
+  const uint32_t waves_per_block = blockDim.x >> 6;
+  const uint32_t total_waves = gridDim.x * waves_per_block;
+  const uint32_t ksteps = a.m / 64u + 1u;  // steps covering i in [0, m]
+  const u32x4 L5 = ocb_l(LB, 2u + 5u);
+  const uint32_t gl = lane ^ (lane >> 1);
+  u32x4 Dl = {0u, 0u, 0u, 0u};
+  for (uint32_t b = 0; b < 6u; ++b)
+    if (gl & (1u << b)) Dl ^= ocb_l(LB, 2u + b);
+
+  for (uint32_t item = blockIdx.x * waves_per_block + (threadIdx.x >> 6); item < a.nitems; item += total_waves) {
+    const uint32_t r = item / a.nchunks;
+    const uint32_t c = item - r * a.nchunks;
+    const uint32_t k0 = c * a.S;
+    const uint32_t k1 = min(k0 + a.S, ksteps);
+    const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
+    uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
+    const u32x4 B = a.off0[r] ^ Dl;
+    u32x4 U = ocb_lsum(LB, ((uint64_t)k0 << 6) ^ ((uint64_t)k0 << 5));
+    u32x4 csum = {0u, 0u, 0u, 0u};
+    for (uint32_t k = k0; k < k1; ++k) {
+      const uint32_t i = 64u * k + lane;  // RFC block index (1-based)
+      const u32x4 off = B ^ U;
+      if (i >= 1u && i <= a.m) {
+        const uint64_t boff = 16ull * (i - 1u);
+        const u32x4 v = *reinterpret_cast<const u32x4a*>(in_rec + boff);
+        u32x4 x = v ^ off;
+        uint32_t s0 = x[0], s1 = x[1], s2 = x[2], s3 = x[3];
+        if (DECRYPT) aes128_dec(a.drk, lbd, lbs, s0, s1, s2, s3);
+        else aes128_enc(a.rk, lbe, s0, s1, s2, s3);
+        const u32x4 y = u32x4{s0, s1, s2, s3} ^ off;
+        *reinterpret_cast<u32x4a*>(out_rec + boff) = y;
+        csum ^= DECRYPT ? y : v;
+      }
+      U ^= L5 ^ ocb_l(LB, 2u + 6u + (uint32_t)__builtin_ctz(k + 1u));
+    }
+#pragma unroll
+    for (int msk = 1; msk < 64; msk <<= 1) csum ^= shfl_xor4(csum, msk);
+    if (lane == 0) a.partial[item] = csum;
+  }
+}
+
+struct OcbFinalArgs {
+  const uint8_t* in;
+  uint8_t* out;
+  const uint8_t* nonces;
+  uint64_t in_stride, out_stride, nonce_stride;
+  uint32_t len, m, nrec, nchunks;
+  const uint32_t* te0;
+  const u32x4* ltab;
+  const u32x4* partial;
+  const u32x4* off0;
+  int32_t* status;   // open: per-record result (internal scratch if the caller passed none)
+  RoundKeys rk;
+};
+
+// One thread per record: checksum reduction, trailing partial block, tag.
+template <bool DECRYPT>
+__global__ __launch_bounds__(256) void ocb_final_kernel(OcbFinalArgs a) {
+  stage_te0(a.te0, 0u);
+  stage_copy(a.ltab, kOcbLSeal, 66u);
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.nrec) return;
+  const uint32_t lb = (threadIdx.x & 31u) << 2;
+  const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
+  uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
+  u32x4 csum = {0u, 0u, 0u, 0u};
+  for (uint32_t c = 0; c < a.nchunks; ++c) csum ^= a.partial[(uint64_t)r * a.nchunks + c];
+  u32x4 off = a.off0[r] ^ ocb_lsum(kOcbLSeal, (uint64_t)a.m ^ ((uint64_t)a.m >> 1));  // Offset_m
+  const uint32_t rem = a.len - 16u * a.m;
+  if (rem) {
+    off ^= ocb_l(kOcbLSeal, 0u);  // Offset_* = Offset_m ^ L_*
+    uint32_t p0 = off[0], p1 = off[1], p2 = off[2], p3 = off[3];
+    aes128_enc(a.rk, lb, p0, p1, p2, p3);  // Pad
+    const u32x4 pad = {p0, p1, p2, p3};
+    const u32x4 v = load_partial(in_rec + 16u * a.m, rem);
+    const u32x4 o = mask_bytes(v ^ pad, rem);
+    store_partial(out_rec + 16u * a.m, o, rem);
+    u32x4 pst = DECRYPT ? o : v;  // P_* || 1 || 0*
+    pst[rem >> 2] |= 0x80u << (8u * (rem & 3u));
+    csum ^= pst;
+  }
+  u32x4 t = csum ^ off ^ ocb_l(kOcbLSeal, 1u);
+  uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
+  aes128_enc(a.rk, lb, t0, t1, t2, t3);
+  const u32x4 tag = {t0, t1, t2, t3};
+  if (!DECRYPT) {
+    uint8_t* tp = out_rec + a.len;
+    if ((a.len & 3u) == 0u) *reinterpret_cast<u32x4a*>(tp) = tag;
+    else store_partial(tp, tag, 16u);
+  } else {
+    const uint8_t* tp = in_rec + a.len;
+    const u32x4 rt = ((a.len & 3u) == 0u) ? *reinterpret_cast<const u32x4a*>(tp) : load_partial(tp, 16u);
+    const u32x4 d = rt ^ tag;
+    a.status[r] = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+  }
+}
+
+// Zero-fill the plaintext of every record whose status is 0 (aead.h:276-278).
+__global__ __launch_bounds__(256) void zero_failed_kernel(uint8_t* out, uint64_t out_stride, uint32_t len,
+                                                          const int32_t* status) {
+  const uint32_t r = blockIdx.x;
+  if (status[r] != 0) return;
+  uint8_t* o = out + (uint64_t)r * out_stride;
+  const uint32_t full = len & ~3u;
+  for (uint32_t i = threadIdx.x * 4u; i < full; i += blockDim.x * 4u) *reinterpret_cast<uint32_t*>(o + i) = 0u;
+  for (uint32_t i = full + threadIdx.x; i < len; i += blockDim.x) o[i] = 0u;
+}
+
+}  // namespace dev
+}  // namespace cmpi

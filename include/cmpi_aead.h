@@ -1,0 +1,143 @@
+/*
+ * cmpi_aead.h — C ABI of the MI355X-native AEAD seal/open engine (libcmpi_aead.so).
+ *
+ * This is the batched replacement for the BoringSSL calls CryptMPI makes on its per-message
+ * hot path.  Plain pointers and sizes only; `stream` is a hipStream_t
+ * passed as void* (NULL = the legacy default stream).  Device-resident entry points take
+ * DEVICE pointers and are asynchronous on `stream`; the *_host entry points take HOST
+ * pointers (pinned for full PCIe rate), stage through the device and are synchronous.
+ *
+ * Reference interfaces each entry point replaces (file:line):
+ *   cmpi_ctx_new(CMPI_AES_128_GCM,…)  EVP_AEAD_CTX_new(EVP_aead_aes_128_gcm(), key, 16, 0)
+ *                         MV/boringssl-master/include/openssl/aead.h:208-212; callers
+ *                         MV/src/mpi/init/init.c:587-612, MV/src/mpi/pt2pt/send.c:588-599
+ *   cmpi_ctx_new(CMPI_AES_128_CTR/ECB) EVP_CIPHER_CTX_new + EVP_EncryptInit_ex(…, EVP_aes_128_ctr|ecb,
+ *                         NULL, key, NULL)  cipher.h:84-86, :123, :158; init.c:619, :716, :842-849
+ *   cmpi_ctx_free         EVP_AEAD_CTX_free aead.h:216 / EVP_CIPHER_CTX_free cipher.h:131
+ *   cmpi_gcm_seal_batch   a batch of EVP_AEAD_CTX_seal, aead.h:256-260; the loops at
+ *                         MV/src/mpi/pt2pt/send.c:292-327 (600), :646-706 / :754-831 (602),
+ *                         MV/src/mpi/coll/alltoall.c:795-811 (naive 1002)
+ *   cmpi_gcm_open_batch   a batch of EVP_AEAD_CTX_open, aead.h:281-285; recv.c:322, :583-613,
+ *                         :745-775, alltoall.c:821-834
+ *   cmpi_ctr_xor          EVP_EncryptInit_ex(ctx,NULL,NULL,NULL,iv)+EVP_EncryptUpdate (CTR),
+ *                         cipher.h:158/:174; send.c:985-1008, :1716-1727, :1805-1808
+ *   cmpi_ctr_keystream    generateCommonEncMask (E_K(IV+i) over zeros), send.c:1162-1266
+ *   cmpi_ecb_encrypt      EVP_EncryptUpdate(ctx_enc, newkey, &len, V, 16), send.c:583
+ *   cmpi_ctx_new_subkey   the 602 sub-key: K' = AES-ECB_K(V) then EVP_AEAD_CTX_new(K'),
+ *                         send.c:572-600, recv.c:549-576
+ *   cmpi_iv_count         IV_Count, send.c:1019-1030
+ *   cmpi_ocb_seal/open_batch  AES-128-OCB (RFC 7253) — README-only "Naive OCB" (402); no
+ *                         reference code exists (OPENSSL_NO_OCB, opensslconf.h:49)
+ *
+ * Conventions (EVP_AEAD_CTX_seal/open, aead.h:236-285): 12-byte nonce, no AAD, 16-byte tag
+ * appended after the ciphertext.  open verifies in constant-time-free batch form: a record
+ * whose tag mismatches gets status 0 and its plaintext output zero-filled (aead.h:276-278).
+ * Contexts are immutable after creation and may be used concurrently from several threads /
+ * streams (aead.h:240-241) as long as each concurrent call passes its own `workspace`
+ * (or calls are serialised on one stream).  Nothing is retained after a call returns.
+ */
+#ifndef CMPI_AEAD_H
+#define CMPI_AEAD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMPI_OK 0
+#define CMPI_EINVAL (-1)  /* bad argument: size, alignment, NULL, wrong algorithm   */
+#define CMPI_EHIP (-2)    /* HIP runtime error (message via cmpi_last_error)         */
+#define CMPI_ENOMEM (-3)  /* device allocation failed                               */
+#define CMPI_EAUTH (-4)   /* *_host open: at least one record failed authentication */
+#define CMPI_ENODEV (-5)  /* no usable GPU                                          */
+
+enum cmpi_alg {
+  CMPI_AES_128_GCM = 1,
+  CMPI_AES_128_OCB = 2,
+  CMPI_AES_128_CTR = 3,
+  CMPI_AES_128_ECB = 4
+};
+
+typedef struct cmpi_ctx cmpi_ctx;
+
+/* Library info / errors. */
+const char *cmpi_version(void);
+const char *cmpi_last_error(void); /* thread-local; "" when none */
+int cmpi_device_count(void);
+
+/* Key context: expands the key schedule and the GHASH / OCB tables on the host once and
+ * uploads them to `device` (HIP ordinal).  key_len must be 16.  tag_len 0 or 16.
+ * Returns NULL on failure (see cmpi_last_error). */
+cmpi_ctx *cmpi_ctx_new(int alg, const uint8_t *key, size_t key_len, size_t tag_len, int device);
+/* 602 sub-key context: K' = AES-128_K(V) computed by the ECB kernel on the device of
+ * `ecb_ctx` (an ECB or GCM context holding K), then a GCM context for K'. */
+cmpi_ctx *cmpi_ctx_new_subkey(const cmpi_ctx *base, const uint8_t v[16]);
+void cmpi_ctx_free(cmpi_ctx *ctx);
+int cmpi_ctx_device(const cmpi_ctx *ctx);
+
+/* ---------------- AES-128-GCM, uniform batches (device pointers) ----------------
+ * Record i (0 <= i < nrec):
+ *   seal: reads  len bytes  of plaintext at in  + i*in_stride,
+ *         writes len+16 bytes ct||tag     at out + i*out_stride,
+ *         nonce  12 bytes                 at nonces + i*nonce_stride.
+ *   open: reads  len+16 bytes ct||tag at in, writes len bytes plaintext at out,
+ *         status[i] = 1 ok / 0 authentication failure (plaintext zero-filled); status may be NULL.
+ * All pointers and strides must be multiples of 4 bytes; len is any value >= 0.  Records must
+ * not overlap each other; out may equal in (in-place) but must not partially overlap it.
+ * The naive-collective wire layout nonce(12)||ct(n)||tag(16) is expressed as
+ *   out = wire + 12, nonces = wire, out_stride = nonce_stride = n + 28.
+ * workspace: NULL (use the context's internal scratch; calls on one ctx then must be
+ * stream-ordered) or a device buffer of cmpi_gcm_workspace_size(len, nrec) bytes. */
+size_t cmpi_gcm_workspace_size(const cmpi_ctx *ctx, size_t len, size_t nrec);
+int cmpi_gcm_seal_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
+                        size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
+                        size_t nrec, void *workspace, void *stream);
+int cmpi_gcm_open_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
+                        size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
+                        size_t nrec, int32_t *status, void *workspace, void *stream);
+
+/* Host-memory variants: H2D (hipMemcpyAsync) -> kernel -> D2H on an internal stream, then
+ * synchronise.  Returns CMPI_OK, CMPI_EAUTH (open: some record failed; status[] on the host
+ * says which, may be NULL) or another error. */
+int cmpi_gcm_seal_host(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
+                       size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
+                       size_t nrec);
+int cmpi_gcm_open_host(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
+                       size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
+                       size_t nrec, int32_t *status);
+
+/* ---------------- AES-128-OCB3 (RFC 7253), uniform batches (device pointers) ----------------
+ * Same record layout and status semantics as the GCM batch calls. */
+size_t cmpi_ocb_workspace_size(const cmpi_ctx *ctx, size_t len, size_t nrec);
+int cmpi_ocb_seal_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
+                        size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
+                        size_t nrec, void *workspace, void *stream);
+int cmpi_ocb_open_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
+                        size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
+                        size_t nrec, int32_t *status, void *workspace, void *stream);
+
+/* ---------------- AES-128-CTR ----------------
+ * out[j] = in[j] XOR E_K(ctr_block + floor(j/16)) for 0 <= j < n, 128-bit big-endian counter
+ * increment (EVP_aes_128_ctr).  ctr_block is a 16-byte HOST array (usually cmpi_iv_count()
+ * of the common IV).  in/out device pointers, 4-byte aligned; in == out allowed. */
+int cmpi_ctr_xor(const cmpi_ctx *ctx, uint8_t *out, const uint8_t *in, size_t n,
+                 const uint8_t ctr_block[16], void *stream);
+/* Materialised keystream: out = E_K(ctr_block + i) for i < nblocks (the mask ring of
+ * generateCommonEncMask). */
+int cmpi_ctr_keystream(const cmpi_ctx *ctx, uint8_t *out, size_t nblocks, const uint8_t ctr_block[16],
+                       void *stream);
+/* IV_Count (send.c:1019-1030), host helper: iv += (uint32_t)cter with CryptMPI's exact carry
+ * behaviour (the carry out of the first byte add is dropped when cter + iv[15] >= 2^32). */
+void cmpi_iv_count(uint8_t iv[16], unsigned long cter);
+void cmpi_iv_count_out(uint8_t iv[16], unsigned long cter, const uint8_t in[16]);
+
+/* ---------------- AES-128-ECB ----------------
+ * out = E_K(in) over nblocks 16-byte blocks (device pointers). */
+int cmpi_ecb_encrypt(const cmpi_ctx *ctx, uint8_t *out, const uint8_t *in, size_t nblocks, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CMPI_AEAD_H */

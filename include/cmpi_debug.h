@@ -1,0 +1,26 @@
+/*
+ * cmpi_debug.h — test hooks of libcmpi_aead.so (not part of the drop-in surface).
+ * Used by tests/ to force every GCM work decomposition onto small inputs.
+ */
+#ifndef CMPI_DEBUG_H
+#define CMPI_DEBUG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cmpi_aead.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Force GCM lanes-per-record (1, 2 or 4; anything else = automatic) and segments per record
+ * (0 = automatic) for every subsequent launch in the process. */
+void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments);
+/* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}. */
+int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,233 @@
+"""AES-128-GCM on the MI355X through the C ABI vs the oracle / golden vectors (bit-exact).
+
+Covers every work decomposition the engine can pick (lanes per record L = 1/2/4, one or many
+segments per record), the CryptMPI record layouts (dense, naive-collective wire
+nonce||ct||tag with stride n+28, in place), the edge sizes (0, partial blocks, 64 KiB-1,
+1 MiB), open's forgery path (status 0 + zero-filled plaintext, aead.h:276-278) and the
+full BASELINE config-2 batch through size-independent properties."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from cryptmpi_2022_amd import aead
+from cryptmpi_2022_amd.synth import random_nonces, records, splitmix64_bytes
+from tests.gpu_util import dev, empty, host, status_buf
+
+pytestmark = pytest.mark.gpu
+
+KEY = bytes.fromhex("000102030405060708090a0b0c0d0e0f")
+
+
+@pytest.fixture(autouse=True)
+def _auto_plan():
+    aead.force_plan(0, 0)
+    yield
+    aead.force_plan(0, 0)
+
+
+def gpu_seal(ctx, nonces: np.ndarray, pt: np.ndarray) -> np.ndarray:
+    nrec, n = pt.shape
+    out = empty(nrec * (n + 16), fill=0xAA)
+    ctx.seal_batch(out, dev(pt), dev(nonces), n, nrec)
+    return host(out).reshape(nrec, n + 16)
+
+
+def gpu_open(ctx, nonces: np.ndarray, ct: np.ndarray):
+    nrec, m = ct.shape
+    n = m - 16
+    out = empty(nrec * n, fill=0xAA)
+    st = status_buf(nrec)
+    ctx.open_batch(out, dev(ct), dev(nonces), n, nrec, status=st)
+    return host(out).reshape(nrec, n), host(st)[:nrec]
+
+
+def test_published_kat(golden):
+    kat, _ = golden
+    for v in kat["gcm"]:
+        if v["aad"]:
+            continue  # CryptMPI never passes AAD; the engine's GCM has none
+        ctx = aead.AeadCtx(bytes.fromhex(v["key"]))
+        pt = np.frombuffer(bytes.fromhex(v["pt"]), np.uint8)[None, :].copy()
+        nonce = np.frombuffer(bytes.fromhex(v["nonce"]), np.uint8)[None, :].copy()
+        out = gpu_seal(ctx, nonce, pt)
+        assert out[0].tobytes().hex() == v["ct"] + v["tag"], v["src"]
+        back, st = gpu_open(ctx, nonce, out)
+        assert st[0] == 1 and back[0].tobytes() == pt[0].tobytes()
+
+
+def test_openssl_vectors(golden):
+    _, ossl = golden
+    ctx = aead.AeadCtx(bytes.fromhex(ossl["key"]))
+    for e in ossl["gcm"]:
+        pt = splitmix64_bytes(e["pt_seed"], e["len"])[None, :]
+        nonce = np.frombuffer(bytes.fromhex(e["nonce"]), np.uint8)[None, :].copy()
+        out = gpu_seal(ctx, nonce, pt)[0].tobytes()
+        if "out" in e:
+            assert out.hex() == e["out"], (e["len"], e["nonce_kind"])
+        else:
+            assert hashlib.sha256(out).hexdigest() == e["out_sha256"], (e["len"], e["nonce_kind"])
+        back, st = gpu_open(ctx, nonce, np.frombuffer(out, np.uint8)[None, :].copy())
+        assert st[0] == 1 and back[0].tobytes() == pt[0].tobytes()
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 31, 48, 100, 1024, 1040, 4096, 4097, 65535])
+@pytest.mark.parametrize("plan", [(0, 0), (1, 1), (2, 1), (4, 1), (4, 3), (1, 2), (2, 7)])
+def test_batch_parity_plans(n, plan):
+    aead.force_plan(*plan)
+    nrec = 24 if n <= 4096 else 4
+    pt = records(0x1000 + n, nrec, n)
+    nonces = random_nonces(0x2000 + n, nrec)
+    ctx = aead.AeadCtx(KEY)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    got = gpu_seal(ctx, nonces, pt)
+    assert np.array_equal(got, want), f"n={n} plan={plan} plan_used={aead.gcm_plan(ctx, n, nrec)}"
+    back, st = gpu_open(ctx, nonces, want)
+    assert (st == 1).all() and np.array_equal(back, pt)
+
+
+def test_auto_plans_cover_all_lane_widths():
+    ctx = aead.AeadCtx(KEY)
+    seen = {aead.gcm_plan(ctx, n, N)[0] for n, N in [(16, 1 << 20), (1024, 200000), (1024, 65536), (64, 16)]}
+    assert seen == {1, 2, 4}
+
+
+def test_wire_layout_naive_alltoall():
+    """alltoall.c:795-834: record i = nonce(12) || ct(n) || tag(16) at i*(n+28)."""
+    n, nrec = 1000, 8
+    stride = n + 28
+    pt = records(77, nrec, n)
+    nonces = random_nonces(78, nrec)
+    wire = np.zeros((nrec, stride), np.uint8)
+    wire[:, :12] = nonces
+    wbuf = dev(wire)
+    ctx = aead.AeadCtx(KEY)
+    ctx.seal_batch(wbuf[12:], dev(pt), wbuf, n, nrec, out_stride=stride, nonce_stride=stride)
+    got = host(wbuf).reshape(nrec, stride)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    assert np.array_equal(got[:, :12], nonces)
+    assert np.array_equal(got[:, 12:], want)
+    # receive side: open straight from the wire
+    out = empty(nrec * n)
+    st = status_buf(nrec)
+    ctx.open_batch(out, wbuf[12:], wbuf, n, nrec, status=st, in_stride=stride, nonce_stride=stride)
+    assert (host(st)[:nrec] == 1).all()
+    assert np.array_equal(host(out).reshape(nrec, n), pt)
+
+
+def test_in_place():
+    n, nrec = 4096, 16
+    pt = records(5, nrec, n)
+    nonces = random_nonces(6, nrec)
+    buf = np.zeros((nrec, n + 16), np.uint8)
+    buf[:, :n] = pt
+    d = dev(buf)
+    ctx = aead.AeadCtx(KEY)
+    ctx.seal_batch(d, d, dev(nonces), n, nrec, in_stride=n + 16, out_stride=n + 16)
+    assert np.array_equal(host(d).reshape(nrec, n + 16), oracle.gcm_seal_batch(KEY, nonces, pt))
+    st = status_buf(nrec)
+    ctx.open_batch(d, d, dev(nonces), n, nrec, status=st, in_stride=n + 16, out_stride=n + 16)
+    assert np.array_equal(host(d).reshape(nrec, n + 16)[:, :n], pt)
+
+
+@pytest.mark.parametrize("plan", [(0, 0), (4, 5), (1, 1)])
+def test_open_forgery(plan):
+    aead.force_plan(*plan)
+    n, nrec = 1024, 32
+    pt = records(9, nrec, n)
+    nonces = random_nonces(10, nrec)
+    ctx = aead.AeadCtx(KEY)
+    ct = oracle.gcm_seal_batch(KEY, nonces, pt)
+    bad = [0, 5, 17, 31]
+    ct[0, 3] ^= 1        # ciphertext bit
+    ct[5, n + 15] ^= 0x80  # tag bit
+    ct[17, n - 1] ^= 4
+    nonces_t = nonces.copy()
+    nonces_t[31, 0] ^= 1  # wrong nonce
+    back, st = gpu_open(ctx, nonces_t, ct)
+    for i in range(nrec):
+        if i in bad:
+            assert st[i] == 0 and not back[i].any(), i
+        else:
+            assert st[i] == 1 and np.array_equal(back[i], pt[i]), i
+
+
+def test_large_records_multisegment():
+    """BASELINE config 5 shape: 8 records of 1 MiB per rank (many segments per record)."""
+    n, nrec = 1 << 20, 8
+    pt = records(0xB16, nrec, n)
+    nonces = random_nonces(0xB17, nrec)
+    ctx = aead.AeadCtx(KEY)
+    L, nseg, G, r0 = aead.gcm_plan(ctx, n, nrec)
+    assert nseg > 1
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    got = gpu_seal(ctx, nonces, pt)
+    assert np.array_equal(got, want)
+    want[3, 100] ^= 1
+    back, st = gpu_open(ctx, nonces, want)
+    assert list(st) == [1, 1, 1, 0, 1, 1, 1, 1]
+    assert not back[3].any() and np.array_equal(back[[0, 1, 2, 4, 5, 6, 7]], pt[[0, 1, 2, 4, 5, 6, 7]])
+
+
+def test_config2_full_batch_properties():
+    """65 536 x 1 KiB (BASELINE config 2): seal->open round trip over the whole batch,
+    every tag unique, and a seeded sample bit-exact against the oracle."""
+    import torch
+
+    n, nrec = 1024, 65536
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    pt = torch.randint(0, 256, (nrec * n,), dtype=torch.uint8, device="cuda", generator=g)
+    nonces = torch.randint(0, 256, (nrec * 12,), dtype=torch.uint8, device="cuda", generator=g)
+    ctx = aead.AeadCtx(KEY)
+    ct = empty(nrec * (n + 16))
+    ctx.seal_batch(ct, pt, nonces, n, nrec)
+    back = empty(nrec * n)
+    st = status_buf(nrec)
+    ctx.open_batch(back, ct, nonces, n, nrec, status=st)
+    torch.cuda.synchronize()
+    assert bool((st == 1).all())
+    assert torch.equal(back, pt)
+    tags = ct.view(nrec, n + 16)[:, n:].cpu().numpy()
+    assert len({t.tobytes() for t in tags}) == nrec
+    idx = np.random.default_rng(0).choice(nrec, 64, replace=False)
+    pt_h = pt.view(nrec, n).cpu().numpy()[idx]
+    nn_h = nonces.view(nrec, 12).cpu().numpy()[idx]
+    want = oracle.gcm_seal_batch(KEY, nn_h, pt_h)
+    assert np.array_equal(ct.view(nrec, n + 16).cpu().numpy()[idx], want)
+
+
+def test_host_staging_api():
+    n, nrec = 777, 20
+    pt = records(3, nrec, n)
+    nonces = random_nonces(4, nrec)
+    ctx = aead.AeadCtx(KEY)
+    got = ctx.seal_host_batch(nonces, pt)
+    assert np.array_equal(got, oracle.gcm_seal_batch(KEY, nonces, pt))
+    back, st = ctx.open_host_batch(nonces, got)
+    assert (st == 1).all() and np.array_equal(back, pt)
+    # EVP_AEAD_CTX_seal/open single-message mirror
+    one = ctx.seal(nonces[0].tobytes(), pt[0].tobytes())
+    assert one == oracle.gcm_seal(KEY, nonces[0].tobytes(), pt[0].tobytes())
+    assert ctx.open(nonces[0].tobytes(), one) == pt[0].tobytes()
+    assert ctx.open(nonces[0].tobytes(), one[:-1] + bytes([one[-1] ^ 1])) is None
+
+
+def test_subkey602_matches_oracle():
+    """602 sub-key (send.c:572-600): K' = AES-ECB_K(V) on the GPU, then GCM under K'."""
+    base = aead.CipherCtx(KEY, "aes-128-ecb")
+    v = splitmix64_bytes(0x602, 16).tobytes()
+    sub = aead.AeadCtx.subkey602(base, v)
+    kprime = oracle.ecb_encrypt(KEY, v)
+    pt = records(11, 4, 300)
+    nonces = np.stack([np.frombuffer(oracle.nonce602(b"0", i), np.uint8) for i in range(4)])
+    assert np.array_equal(gpu_seal(sub, nonces, pt), oracle.gcm_seal_batch(kprime, nonces, pt))
+
+
+def test_rejects_misaligned():
+    ctx = aead.AeadCtx(KEY)
+    buf = empty(4096)
+    with pytest.raises(Exception):
+        ctx.seal_batch(buf[1:], buf, buf, 16, 2)
+    with pytest.raises(Exception):
+        ctx.seal_batch(buf, buf, buf, 16, 2, out_stride=34)
