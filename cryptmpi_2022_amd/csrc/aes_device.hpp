@@ -21,10 +21,12 @@ namespace dev {
 extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// Under-aligned (4-byte) 16-byte vector for record data: records may start at any 4-byte
-// offset (e.g. the nonce(12)||ct||tag wire layout).  gfx950 global_load/store_dwordx4 accept
-// dword-aligned addresses.
-typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+// Byte-aligned 16-byte / 4-byte views of record data: records may start at any byte offset
+// (the nonce(12)||ct||tag wire layout with odd n, the 602 5-byte segment prefix).  On gfx950
+// under amdhsa the backend runs in unaligned-access mode and still emits one
+// global_load/store_dwordx4 (resp. _dword) for these.
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32a __attribute__((aligned(1)));
 
 // LDS accesses by raw byte offset.  All kernels here use only dynamic LDS (no static
 // __shared__), so the dynamic region starts at LDS address 0 and an offset IS the address:

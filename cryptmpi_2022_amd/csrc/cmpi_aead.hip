@@ -111,8 +111,6 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
   return CMPI_OK;
 }
 
-bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
-
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device).
 std::mutex g_attr_mu;
 std::map<std::pair<const void*, int>, int> g_attr_done;
@@ -209,10 +207,8 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   if (!c) return fail(CMPI_EINVAL, "null ctx");
   if (c->alg != CMPI_AES_128_GCM) return fail(CMPI_EINVAL, "ctx is not AES-128-GCM");
   if (nrec == 0) return CMPI_OK;
-  if (!out || !in || !nonces) return fail(CMPI_EINVAL, "null buffer");
-  if (!aligned4(out) || !aligned4(in) || !aligned4(nonces) || (out_stride & 3) || (in_stride & 3) ||
-      (nonce_stride & 3))
-    return fail(CMPI_EINVAL, "pointers and strides must be 4-byte aligned");
+  if (!out || !nonces || (!in && (DEC || len))) return fail(CMPI_EINVAL, "null buffer");
+  if (!in) in = out;  // seal of empty records reads nothing
   if (len > 0xFFFFFFF0ull || nrec > 0x7FFFFFFFull) return fail(CMPI_EINVAL, "len/nrec out of range");
   const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
   if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
@@ -311,10 +307,8 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   if (!c) return fail(CMPI_EINVAL, "null ctx");
   if (c->alg != CMPI_AES_128_OCB) return fail(CMPI_EINVAL, "ctx is not AES-128-OCB");
   if (nrec == 0) return CMPI_OK;
-  if (!out || !in || !nonces) return fail(CMPI_EINVAL, "null buffer");
-  if (!aligned4(out) || !aligned4(in) || !aligned4(nonces) || (out_stride & 3) || (in_stride & 3) ||
-      (nonce_stride & 3))
-    return fail(CMPI_EINVAL, "pointers and strides must be 4-byte aligned");
+  if (!out || !nonces || (!in && (DEC || len))) return fail(CMPI_EINVAL, "null buffer");
+  if (!in) in = out;  // seal of empty records reads nothing
   if (len > 0xFFFFFFF0ull || nrec > 0x7FFFFFFFull) return fail(CMPI_EINVAL, "len/nrec out of range");
   const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
   if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
@@ -416,7 +410,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
     return fail(CMPI_EINVAL, "stride smaller than record");
   DeviceGuard dg(c->device);
-  std::lock_guard<std::mutex> lk(c->mu);  // staging buffers are per ctx
+  std::unique_lock<std::mutex> lk(c->mu);  // staging buffers are per ctx
   if (!c->hstream) HIP_TRY(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t ip = up16(in_rec), op = up16(out_rec);
@@ -430,12 +424,12 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   hipStream_t s = c->hstream;
   if (in_rec) HIP_TRY(hipMemcpy2DAsync(d_in, ip, in, nrec > 1 ? in_stride : in_rec, in_rec, nrec, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpy2DAsync(d_n, 16, nonces, nrec > 1 ? nonce_stride : 12, 12, nrec, hipMemcpyHostToDevice, s));
-  c->mu.unlock();  // the batch call takes the lock itself for its scratch
+  lk.unlock();  // the batch call takes the lock itself for its scratch
   if (OCB)
     rc = ocb_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nrec, DEC ? d_st : nullptr, nullptr, s);
   else
     rc = gcm_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nrec, DEC ? d_st : nullptr, nullptr, s);
-  c->mu.lock();
+  lk.lock();
   if (rc) return rc;
   if (out_rec) HIP_TRY(hipMemcpy2DAsync(out, nrec > 1 ? out_stride : out_rec, d_out, op, out_rec, nrec, hipMemcpyDeviceToHost, s));
   std::vector<int32_t> hst;
@@ -450,6 +444,52 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     if (status) memcpy(status, hst.data(), 4 * nrec);
     if (bad) return fail(CMPI_EAUTH, "%zu of %zu records failed authentication", bad, nrec);
   }
+  return CMPI_OK;
+}
+
+int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, const uint8_t ctr[16],
+                      void* stream) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (c->alg != CMPI_AES_128_CTR && c->alg != CMPI_AES_128_GCM && c->alg != CMPI_AES_128_ECB)
+    return fail(CMPI_EINVAL, "ctx algorithm cannot run CTR");
+  if (!ctr || !out) return fail(CMPI_EINVAL, "null argument");
+  if (n == 0) return CMPI_OK;
+  DeviceGuard dg(c->device);
+  cmpi::dev::CtrArgs a{};
+  a.in = in;
+  a.out = out;
+  a.n = n;
+  a.nblk = (n + 15) / 16;
+  a.ctr_hi = cmpi::be64(ctr);
+  a.ctr_lo = cmpi::be64(ctr + 8);
+  a.te0 = c->dt->te0;
+  a.rk = c->rk;
+  const uint64_t blocks = (a.nblk + 511) / 512;  // 2 blocks per thread per pass
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 4));
+  hipStream_t st = (hipStream_t)stream;
+  if (in) hipLaunchKernelGGL(cmpi::dev::ctr_kernel<true>, dim3(grid), dim3(256), 32768, st, a);
+  else hipLaunchKernelGGL(cmpi::dev::ctr_kernel<false>, dim3(grid), dim3(256), 32768, st, a);
+  HIP_TRY(hipGetLastError());
+  return CMPI_OK;
+}
+
+// Stage host bytes into the ctx's device buffer at byte offset `pad`, run `fn(dev_in, dev_out)`
+// on the internal stream, copy [pad, pad+n) back.  Serialised per ctx.
+template <typename F>
+int host_stream_op(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, unsigned pad, F fn) {
+  DeviceGuard dg(c->device);
+  std::unique_lock<std::mutex> lk(c->mu);
+  if (!c->hstream) HIP_TRY(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
+  const size_t span = ((size_t)pad + n + 15) & ~(size_t)15;
+  int rc = ensure_buf((void**)&c->stage, &c->stage_cap, 2 * span);
+  if (rc) return rc;
+  uint8_t* d_in = c->stage;
+  uint8_t* d_out = c->stage + span;
+  HIP_TRY(hipMemcpyAsync(d_in + pad, in, n, hipMemcpyHostToDevice, c->hstream));
+  rc = fn(d_in, d_out, span, c->hstream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out, d_out + pad, n, hipMemcpyDeviceToHost, c->hstream));
+  HIP_TRY(hipStreamSynchronize(c->hstream));
   return CMPI_OK;
 }
 
@@ -615,31 +655,14 @@ int cmpi_ocb_open_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, cons
                          stream);
 }
 
-static int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, const uint8_t ctr[16],
-                      void* stream) {
-  if (!c) return fail(CMPI_EINVAL, "null ctx");
-  if (c->alg != CMPI_AES_128_CTR && c->alg != CMPI_AES_128_GCM && c->alg != CMPI_AES_128_ECB)
-    return fail(CMPI_EINVAL, "ctx algorithm cannot run CTR");
-  if (!ctr || !out) return fail(CMPI_EINVAL, "null argument");
-  if (n == 0) return CMPI_OK;
-  if (!aligned4(out) || (in && !aligned4(in))) return fail(CMPI_EINVAL, "pointers must be 4-byte aligned");
-  DeviceGuard dg(c->device);
-  cmpi::dev::CtrArgs a{};
-  a.in = in;
-  a.out = out;
-  a.n = n;
-  a.nblk = (n + 15) / 16;
-  a.ctr_hi = cmpi::be64(ctr);
-  a.ctr_lo = cmpi::be64(ctr + 8);
-  a.te0 = c->dt->te0;
-  a.rk = c->rk;
-  const uint64_t blocks = (a.nblk + 511) / 512;  // 2 blocks per thread per pass
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 4));
-  hipStream_t st = (hipStream_t)stream;
-  if (in) hipLaunchKernelGGL(cmpi::dev::ctr_kernel<true>, dim3(grid), dim3(256), 32768, st, a);
-  else hipLaunchKernelGGL(cmpi::dev::ctr_kernel<false>, dim3(grid), dim3(256), 32768, st, a);
-  HIP_TRY(hipGetLastError());
-  return CMPI_OK;
+int cmpi_ocb_seal_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                       const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec) {
+  return aead_host<false, true>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, nullptr);
+}
+
+int cmpi_ocb_open_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                       const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status) {
+  return aead_host<true, true>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, status);
 }
 
 int cmpi_ctr_xor(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, const uint8_t ctr_block[16],
@@ -650,6 +673,24 @@ int cmpi_ctr_xor(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, c
 
 int cmpi_ctr_keystream(const cmpi_ctx* c, uint8_t* out, size_t nblocks, const uint8_t ctr_block[16], void* stream) {
   return ctr_launch(c, out, nullptr, nblocks * 16, ctr_block, stream);
+}
+
+int cmpi_ctr_xor_host(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, const uint8_t ctr_block[16],
+                      unsigned skip) {
+  if (!c || !out || !in || !ctr_block) return fail(CMPI_EINVAL, "null argument");
+  if (skip > 15) return fail(CMPI_EINVAL, "skip must be 0..15");
+  if (n == 0) return CMPI_OK;
+  return host_stream_op(c, out, in, n, skip, [&](uint8_t* di, uint8_t* dout, size_t span, hipStream_t s) {
+    return ctr_launch(c, dout, di, (size_t)skip + n, ctr_block, s);
+  });
+}
+
+int cmpi_ecb_encrypt_host(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t nblocks) {
+  if (!c || !out || !in) return fail(CMPI_EINVAL, "null argument");
+  if (nblocks == 0) return CMPI_OK;
+  return host_stream_op(c, out, in, nblocks * 16, 0, [&](uint8_t* di, uint8_t* dout, size_t span, hipStream_t s) {
+    return cmpi_ecb_encrypt(c, dout, di, nblocks, s);
+  });
 }
 
 void cmpi_iv_count(uint8_t iv[16], unsigned long cter) {
@@ -676,7 +717,6 @@ int cmpi_ecb_encrypt(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t 
   if (!c) return fail(CMPI_EINVAL, "null ctx");
   if (!out || !in) return fail(CMPI_EINVAL, "null buffer");
   if (nblocks == 0) return CMPI_OK;
-  if (!aligned4(out) || !aligned4(in)) return fail(CMPI_EINVAL, "pointers must be 4-byte aligned");
   DeviceGuard dg(c->device);
   cmpi::dev::EcbArgs a{};
   a.in = in;

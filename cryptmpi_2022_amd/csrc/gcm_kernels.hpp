@@ -72,7 +72,7 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
     const uint32_t nslots = nxs + (s == 0 ? 1u : 0u);  // + the J0 slot
     const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
     uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
-    const uint32_t* np = reinterpret_cast<const uint32_t*>(a.nonces + (uint64_t)r * a.nonce_stride);
+    const u32a* np = reinterpret_cast<const u32a*>(a.nonces + (uint64_t)r * a.nonce_stride);
     const uint32_t n0 = np[0], n1 = np[1], n2 = np[2];
 
     u32x4 acc = {0u, 0u, 0u, 0u};
@@ -138,14 +138,13 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
     if (!DECRYPT) {
       if (q == 0) {
         uint8_t* tp = out_rec + a.len;
-        if ((a.len & 3u) == 0u) st_blk(tp, f);
-        else store_partial(tp, f, 16u);
+        st_blk(tp, f);
       }
     } else {
       int ok = 1;
       if (q == 0) {
         const uint8_t* tp = in_rec + a.len;
-        const u32x4 t = ((a.len & 3u) == 0u) ? ld_blk(tp) : load_partial(tp, 16u);
+        const u32x4 t = ld_blk(tp);
         const u32x4 d = t ^ f;
         ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
         if (a.status) a.status[r] = ok;
@@ -193,14 +192,13 @@ __global__ __launch_bounds__(64) void gcm_combine_kernel(GcmCombineArgs a) {
   if (!DECRYPT) {
     if (lane == 0) {
       uint8_t* tp = a.out + (uint64_t)r * a.out_stride + a.len;
-      if ((a.len & 3u) == 0u) st_blk(tp, y);
-      else store_partial(tp, y, 16u);
+      st_blk(tp, y);
     }
     return;
   }
   if (lane == 0) {
     const uint8_t* tp = a.in + (uint64_t)r * a.in_stride + a.len;
-    const u32x4 t = ((a.len & 3u) == 0u) ? ld_blk(tp) : load_partial(tp, 16u);
+    const u32x4 t = ld_blk(tp);
     const u32x4 d = t ^ y;
     ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
     if (a.status) a.status[r] = ok;
@@ -209,7 +207,7 @@ __global__ __launch_bounds__(64) void gcm_combine_kernel(GcmCombineArgs a) {
   if (!ok) {
     uint8_t* o = a.out + (uint64_t)r * a.out_stride;
     const uint32_t full = a.len & ~3u;
-    for (uint32_t i = lane * 4u; i < full; i += 64u * 4u) *reinterpret_cast<uint32_t*>(o + i) = 0u;
+    for (uint32_t i = lane * 4u; i < full; i += 64u * 4u) *reinterpret_cast<u32a*>(o + i) = 0u;
     for (uint32_t i = full + lane; i < a.len; i += 64u) o[i] = 0u;
   }
 }

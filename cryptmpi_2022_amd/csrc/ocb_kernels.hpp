@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void ocb_offset_kernel(OcbOffsetArgs a) {
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.nrec) return;
-  const uint32_t* np = reinterpret_cast<const uint32_t*>(a.nonces + (uint64_t)r * a.nonce_stride);
+  const u32a* np = reinterpret_cast<const u32a*>(a.nonces + (uint64_t)r * a.nonce_stride);
   a.off0[r] = ocb_offset0(a.rk, (threadIdx.x & 31u) << 2, np[0], np[1], np[2]);
 }
 
@@ -196,11 +196,10 @@ __global__ __launch_bounds__(256) void ocb_final_kernel(OcbFinalArgs a) {
   const u32x4 tag = {t0, t1, t2, t3};
   if (!DECRYPT) {
     uint8_t* tp = out_rec + a.len;
-    if ((a.len & 3u) == 0u) *reinterpret_cast<u32x4a*>(tp) = tag;
-    else store_partial(tp, tag, 16u);
+    *reinterpret_cast<u32x4a*>(tp) = tag;
   } else {
     const uint8_t* tp = in_rec + a.len;
-    const u32x4 rt = ((a.len & 3u) == 0u) ? *reinterpret_cast<const u32x4a*>(tp) : load_partial(tp, 16u);
+    const u32x4 rt = *reinterpret_cast<const u32x4a*>(tp);
     const u32x4 d = rt ^ tag;
     a.status[r] = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
   }
@@ -213,7 +212,7 @@ __global__ __launch_bounds__(256) void zero_failed_kernel(uint8_t* out, uint64_t
   if (status[r] != 0) return;
   uint8_t* o = out + (uint64_t)r * out_stride;
   const uint32_t full = len & ~3u;
-  for (uint32_t i = threadIdx.x * 4u; i < full; i += blockDim.x * 4u) *reinterpret_cast<uint32_t*>(o + i) = 0u;
+  for (uint32_t i = threadIdx.x * 4u; i < full; i += blockDim.x * 4u) *reinterpret_cast<u32a*>(o + i) = 0u;
   for (uint32_t i = full + threadIdx.x; i < len; i += blockDim.x) o[i] = 0u;
 }
 

@@ -109,7 +109,7 @@ int cmpi_gcm_open_host(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, con
                        size_t nrec, int32_t *status);
 
 /* ---------------- AES-128-OCB3 (RFC 7253), uniform batches (device pointers) ----------------
- * Same record layout and status semantics as the GCM batch calls. */
+ * Same record layout and status semantics as the GCM batch calls (+ host-memory variants). */
 size_t cmpi_ocb_workspace_size(const cmpi_ctx *ctx, size_t len, size_t nrec);
 int cmpi_ocb_seal_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
                         size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
@@ -117,6 +117,12 @@ int cmpi_ocb_seal_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, co
 int cmpi_ocb_open_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
                         size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
                         size_t nrec, int32_t *status, void *workspace, void *stream);
+int cmpi_ocb_seal_host(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
+                       size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
+                       size_t nrec);
+int cmpi_ocb_open_host(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
+                       size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
+                       size_t nrec, int32_t *status);
 
 /* ---------------- AES-128-CTR ----------------
  * out[j] = in[j] XOR E_K(ctr_block + floor(j/16)) for 0 <= j < n, 128-bit big-endian counter
@@ -128,6 +134,11 @@ int cmpi_ctr_xor(const cmpi_ctx *ctx, uint8_t *out, const uint8_t *in, size_t n,
  * generateCommonEncMask). */
 int cmpi_ctr_keystream(const cmpi_ctx *ctx, uint8_t *out, size_t nblocks, const uint8_t ctr_block[16],
                        void *stream);
+/* Host-memory CTR (synchronous): like cmpi_ctr_xor, but the first `skip` (0..15) bytes of the
+ * first keystream block are discarded — the continuation state an EVP CTR context keeps
+ * between EVP_EncryptUpdate calls. */
+int cmpi_ctr_xor_host(const cmpi_ctx *ctx, uint8_t *out, const uint8_t *in, size_t n,
+                      const uint8_t ctr_block[16], unsigned skip);
 /* IV_Count (send.c:1019-1030), host helper: iv += (uint32_t)cter with CryptMPI's exact carry
  * behaviour (the carry out of the first byte add is dropped when cter + iv[15] >= 2^32). */
 void cmpi_iv_count(uint8_t iv[16], unsigned long cter);
@@ -136,6 +147,7 @@ void cmpi_iv_count_out(uint8_t iv[16], unsigned long cter, const uint8_t in[16])
 /* ---------------- AES-128-ECB ----------------
  * out = E_K(in) over nblocks 16-byte blocks (device pointers). */
 int cmpi_ecb_encrypt(const cmpi_ctx *ctx, uint8_t *out, const uint8_t *in, size_t nblocks, void *stream);
+int cmpi_ecb_encrypt_host(const cmpi_ctx *ctx, uint8_t *out, const uint8_t *in, size_t nblocks);
 
 #ifdef __cplusplus
 }

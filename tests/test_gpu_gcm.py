@@ -224,10 +224,33 @@ def test_subkey602_matches_oracle():
     assert np.array_equal(gpu_seal(sub, nonces, pt), oracle.gcm_seal_batch(kprime, nonces, pt))
 
 
-def test_rejects_misaligned():
+@pytest.mark.parametrize("n,off,pad", [(17, 1, 3), (1000, 5, 7), (4096, 3, 1), (33, 2, 0)])
+def test_unaligned_records(n, off, pad):
+    """Records at arbitrary byte offsets / odd strides (wire layouts with odd n, the 602 5-byte
+    segment prefix): the engine reads and writes them in place."""
+    nrec = 12
+    in_stride, out_stride, n_stride = n + pad, n + 16 + pad + 1, 12 + pad
+    pt = records(31 + n, nrec, n)
+    nonces = random_nonces(32 + n, nrec)
+    inbuf = np.zeros(off + nrec * in_stride, np.uint8)
+    nbuf = np.zeros(off + nrec * n_stride, np.uint8)
+    for i in range(nrec):
+        inbuf[off + i * in_stride: off + i * in_stride + n] = pt[i]
+        nbuf[off + i * n_stride: off + i * n_stride + 12] = nonces[i]
+    outsz = off + nrec * out_stride
+    d_out = empty(outsz, fill=0x77)
     ctx = aead.AeadCtx(KEY)
-    buf = empty(4096)
-    with pytest.raises(Exception):
-        ctx.seal_batch(buf[1:], buf, buf, 16, 2)
-    with pytest.raises(Exception):
-        ctx.seal_batch(buf, buf, buf, 16, 2, out_stride=34)
+    ctx.seal_batch(d_out[off:], dev(inbuf)[off:], dev(nbuf)[off:], n, nrec, in_stride=in_stride,
+                   out_stride=out_stride, nonce_stride=n_stride)
+    got = host(d_out)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    for i in range(nrec):
+        assert got[off + i * out_stride: off + i * out_stride + n + 16].tobytes() == want[i].tobytes(), i
+        gap = got[off + i * out_stride + n + 16: off + (i + 1) * out_stride]
+        assert (gap == 0x77).all()  # bytes between records untouched
+    back = empty(off + nrec * in_stride, fill=0)
+    st = status_buf(nrec)
+    ctx.open_batch(back[off:], d_out[off:], dev(nbuf)[off:], n, nrec, status=st, in_stride=out_stride,
+                   out_stride=in_stride, nonce_stride=n_stride)
+    assert (host(st)[:nrec] == 1).all()
+    assert np.array_equal(host(back), inbuf)
