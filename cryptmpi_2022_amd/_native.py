@@ -59,10 +59,15 @@ _SIGS = {
     "cmpi_ocb_open_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P, _P], _I),
     "cmpi_ctr_xor": ([_P, _P, _P, _S, _P, _P], _I),
     "cmpi_ctr_keystream": ([_P, _P, _S, _P, _P], _I),
+    "cmpi_ctr_xor_host": ([_P, _P, _P, _S, _P, ctypes.c_uint], _I),
+    "cmpi_ecb_encrypt_host": ([_P, _P, _P, _S], _I),
+    "cmpi_ocb_seal_host": ([_P, _P, _S, _P, _S, _P, _S, _S, _S], _I),
+    "cmpi_ocb_open_host": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P], _I),
     "cmpi_iv_count": ([_P, ctypes.c_ulong], None),
     "cmpi_iv_count_out": ([_P, ctypes.c_ulong, _P], None),
     "cmpi_ecb_encrypt": ([_P, _P, _P, _S, _P], _I),
     "cmpi_debug_force_plan": ([_I, _U32], None),
+    "cmpi_debug_set_gcm_unroll": ([_I], None),
     "cmpi_debug_gcm_plan": ([_P, _S, _S, _P], _I),
 }
 

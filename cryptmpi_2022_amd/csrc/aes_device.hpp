@@ -1,24 +1,29 @@
 // aes_device.hpp — CDNA4 (gfx950) device primitives: LDS-staged AES-128 T-table rounds and
 // table-driven GF(2^128) multiplication, all in the little-endian word convention of
-// aes_tables.hpp.
+// aes_tables.hpp (a block = 4 LE words, word c = AES state column c, row r at bits 8r..8r+7).
 //
-// LDS images (byte offsets inside the kernel's dynamic LDS):
-//  * Te0, 32-way replicated: entry x of replica k at tbase + x*128 + k*4.  Lane l reads replica
-//    (l & 31): in a ds_read_b32 (two 32-lane halves, bank = (addr/4) mod 32) every lane of a half
-//    hits its own bank whatever x is, so AES lookups are bank-conflict free.  tbase must be a
-//    multiple of 32 KiB so the lane term ORs in (x*128 < 32 KiB).
-//  * GHASH byte table (multiplier P): entry (p, v) = (byte p := v)·P at p*4096 + v*16, 64 KiB
-//    at LDS offset 0 so p*4096 folds into the ds_read_b128 immediate offset.
-//  * GHASH nibble tables: 8 KiB each, entry (2p+h, v) at base + p*512 + h*256 + v*16, bases
-//    multiples of 8 KiB so the (p, h) part folds into the immediate and the value term ORs in.
+// LDS images (byte offsets inside the kernel's dynamic LDS; dynamic LDS starts at address 0):
+//  * AES "row image" (64 KiB, base a multiple of 64 KiB): row x at base + x*256 holds
+//    [ Te0[x] x32 replicas | Te1[x] x32 replicas ], Te1 = rotl8(Te0).  Lane l reads replica
+//    (l & 31), so in a ds_read_b32 (two 32-lane halves, bank = (addr/4) mod 32) every lane of a
+//    half sits on its own bank whatever x is: conflict free.  Because rows are 256 B apart the
+//    lookup address is   byte0 = (l&31)*4 (+128 for Te1), byte1 = x, byte2..3 = base >> 16
+//    — ONE v_perm_b32 gathers it from the state word and a lane constant (no shift/mask pair).
+//    With Te2 = rotl16(Te0), Te3 = rotl16(Te1) a column is Te0[a]^Te1[b]^rotl16(Te0[c]^Te1[d]):
+//    8 VALU ops per column instead of 13.  The decryption image is the same with Td0/Td1.
+//  * Inverse S-box image (32 KiB, old style): Si[x] (byte 0 of a word) at base + x*128 + (l&31)*4.
+//  * GHASH byte table (multiplier P, 64 KiB at LDS 0): entry (v, p) = (byte p := v)·P at
+//    v*256 + p*16.  Lane l visits the 16 byte positions in the rotated order p = (t + l) mod 16,
+//    so at every step the 16 lanes of a ds_read_b128 group (whose l mod 16 are all distinct)
+//    hit 16 different 16-byte slots: conflict free.  The address is again one v_perm_b32
+//    (byte0 = p*16 from a packed lane constant, byte1 = v).
+//  * GHASH nibble tables (8 KiB each, rarely used): entry (2p+h, v) at base + p*512 + h*256 + v*16.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace cmpi {
 namespace dev {
-
-extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Byte-aligned 16-byte / 4-byte views of record data: records may start at any byte offset
@@ -28,10 +33,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(1)));
 typedef uint32_t u32a __attribute__((aligned(1)));
 
-// LDS accesses by raw byte offset.  All kernels here use only dynamic LDS (no static
-// __shared__), so the dynamic region starts at LDS address 0 and an offset IS the address:
-// building address_space(3) pointers from the offset lets ds_read use it directly (going
-// through `smem + off` costs an extra v_add per lookup).
+// LDS accesses by raw byte offset: all kernels here use only dynamic LDS (no static
+// __shared__), so an offset IS the LDS address and ds_read uses it directly.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 __device__ __forceinline__ uint32_t lds32(uint32_t off) { return *(const lds_u32*)(size_t)off; }
@@ -41,103 +44,93 @@ __device__ __forceinline__ void lds_st128(uint32_t off, u32x4 v) { *(lds_u32x4*)
 
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
 __device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
-__device__ __forceinline__ uint32_t rotl24(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 8); }
 // gfx950 v_bitop3_b32 with LUT 0x96 = a ^ b ^ c in one VALU op (no v_xor3 on CDNA).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+// v_perm_b32: result byte i = byte sel.byte[i] of {a (bytes 4..7), b (bytes 0..3)}, 0x0c -> 0x00.
+__device__ __forceinline__ uint32_t perm(uint32_t a, uint32_t b, uint32_t sel) { return __builtin_amdgcn_perm(a, b, sel); }
 
-// (byte r of w) * 128, the Te0 row offset
-__device__ __forceinline__ uint32_t tb0(uint32_t w) { return (w << 7) & 0x7f80u; }
-__device__ __forceinline__ uint32_t tb1(uint32_t w) { return (w >> 1) & 0x7f80u; }
-__device__ __forceinline__ uint32_t tb2(uint32_t w) { return (w >> 9) & 0x7f80u; }
-__device__ __forceinline__ uint32_t tb3(uint32_t w) { return (w >> 17) & 0x7f80u; }
+// Row-image address of (byte r of s): byte0/2/3 from the lane constant lb, byte1 = s.byte[r].
+template <int R>
+__device__ __forceinline__ uint32_t ra(uint32_t s, uint32_t lb) {
+  return perm(s, lb, 0x03020400u | ((uint32_t)R << 8));
+}
 
 struct RoundKeys {
   uint32_t w[44];
 };
 
-// One full AES-128 encryption of the block (s0..s3), round keys wave-uniform (kernarg → SGPRs),
-// lb = tbase | (lane & 31) * 4.
-__device__ __forceinline__ void aes128_enc(const RoundKeys& k, uint32_t lb, uint32_t& s0, uint32_t& s1,
+// Lane constants of a row image at `base` (multiple of 64 KiB): Te0/Td0 half and Te1/Td1 half.
+struct RowLanes {
+  uint32_t l0, l1;
+};
+__device__ __forceinline__ RowLanes row_lanes(uint32_t base) {
+  const uint32_t l = ((threadIdx.x & 31u) << 2) | base;
+  return RowLanes{l, l | 128u};
+}
+
+// One AES-128 encryption round (rounds 1..9) on state s, encryption row image.
+__device__ __forceinline__ void enc_round(const RowLanes& L, uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                          uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  const uint32_t a0 = lds32(ra<0>(s0, L.l0)), a1 = lds32(ra<1>(s1, L.l1)), a2 = lds32(ra<2>(s2, L.l0)), a3 = lds32(ra<3>(s3, L.l1));
+  const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l1)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l1));
+  const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l1)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l1));
+  const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l1)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l1));
+  s0 = xor3(a0, a1, k0) ^ rotl16(a2 ^ a3);
+  s1 = xor3(b0, b1, k1) ^ rotl16(b2 ^ b3);
+  s2 = xor3(c0, c1, k2) ^ rotl16(c2 ^ c3);
+  s3 = xor3(d0, d1, k3) ^ rotl16(d2 ^ d3);
+}
+
+// Last encryption round: S[x] = byte 1 of Te0[x]; gather byte 1 of the four lookups per column.
+__device__ __forceinline__ void enc_last(const RowLanes& L, uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                         uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  const uint32_t a0 = lds32(ra<0>(s0, L.l0)), a1 = lds32(ra<1>(s1, L.l0)), a2 = lds32(ra<2>(s2, L.l0)), a3 = lds32(ra<3>(s3, L.l0));
+  const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l0)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l0));
+  const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l0)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l0));
+  const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l0)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l0));
+  s0 = xor3(perm(a1, a0, 0x0c0c0501u), perm(a3, a2, 0x05010c0cu), k0);
+  s1 = xor3(perm(b1, b0, 0x0c0c0501u), perm(b3, b2, 0x05010c0cu), k1);
+  s2 = xor3(perm(c1, c0, 0x0c0c0501u), perm(c3, c2, 0x05010c0cu), k2);
+  s3 = xor3(perm(d1, d0, 0x0c0c0501u), perm(d3, d2, 0x05010c0cu), k3);
+}
+
+// Full AES-128 encryption of (s0..s3); round keys wave-uniform (kernarg -> SGPRs).
+__device__ __forceinline__ void aes128_enc(const RoundKeys& k, const RowLanes& L, uint32_t& s0, uint32_t& s1,
                                            uint32_t& s2, uint32_t& s3) {
   s0 ^= k.w[0];
   s1 ^= k.w[1];
   s2 ^= k.w[2];
   s3 ^= k.w[3];
 #pragma unroll
-  for (int r = 1; r < 10; ++r) {
-    uint32_t a0 = lds32(tb0(s0) | lb), a1 = lds32(tb1(s1) | lb), a2 = lds32(tb2(s2) | lb), a3 = lds32(tb3(s3) | lb);
-    uint32_t b0 = lds32(tb0(s1) | lb), b1 = lds32(tb1(s2) | lb), b2 = lds32(tb2(s3) | lb), b3 = lds32(tb3(s0) | lb);
-    uint32_t c0 = lds32(tb0(s2) | lb), c1 = lds32(tb1(s3) | lb), c2 = lds32(tb2(s0) | lb), c3 = lds32(tb3(s1) | lb);
-    uint32_t d0 = lds32(tb0(s3) | lb), d1 = lds32(tb1(s0) | lb), d2 = lds32(tb2(s1) | lb), d3 = lds32(tb3(s2) | lb);
-    s0 = xor3(xor3(a0, rotl8(a1), rotl16(a2)), rotl24(a3), k.w[4 * r + 0]);
-    s1 = xor3(xor3(b0, rotl8(b1), rotl16(b2)), rotl24(b3), k.w[4 * r + 1]);
-    s2 = xor3(xor3(c0, rotl8(c1), rotl16(c2)), rotl24(c3), k.w[4 * r + 2]);
-    s3 = xor3(xor3(d0, rotl8(d1), rotl16(d2)), rotl24(d3), k.w[4 * r + 3]);
-  }
-  // last round: S[x] = byte 1 of Te0[x]; gather byte 1 of the four lookups per column
-  uint32_t a0 = lds32(tb0(s0) | lb), a1 = lds32(tb1(s1) | lb), a2 = lds32(tb2(s2) | lb), a3 = lds32(tb3(s3) | lb);
-  uint32_t b0 = lds32(tb0(s1) | lb), b1 = lds32(tb1(s2) | lb), b2 = lds32(tb2(s3) | lb), b3 = lds32(tb3(s0) | lb);
-  uint32_t c0 = lds32(tb0(s2) | lb), c1 = lds32(tb1(s3) | lb), c2 = lds32(tb2(s0) | lb), c3 = lds32(tb3(s1) | lb);
-  uint32_t d0 = lds32(tb0(s3) | lb), d1 = lds32(tb1(s0) | lb), d2 = lds32(tb2(s1) | lb), d3 = lds32(tb3(s2) | lb);
-  s0 = xor3(__builtin_amdgcn_perm(a1, a0, 0x0c0c0501u), __builtin_amdgcn_perm(a3, a2, 0x05010c0cu), k.w[40]);
-  s1 = xor3(__builtin_amdgcn_perm(b1, b0, 0x0c0c0501u), __builtin_amdgcn_perm(b3, b2, 0x05010c0cu), k.w[41]);
-  s2 = xor3(__builtin_amdgcn_perm(c1, c0, 0x0c0c0501u), __builtin_amdgcn_perm(c3, c2, 0x05010c0cu), k.w[42]);
-  s3 = xor3(__builtin_amdgcn_perm(d1, d0, 0x0c0c0501u), __builtin_amdgcn_perm(d3, d2, 0x05010c0cu), k.w[43]);
+  for (int r = 1; r < 10; ++r) enc_round(L, s0, s1, s2, s3, k.w[4 * r], k.w[4 * r + 1], k.w[4 * r + 2], k.w[4 * r + 3]);
+  enc_last(L, s0, s1, s2, s3, k.w[40], k.w[41], k.w[42], k.w[43]);
 }
 
-// Two independent blocks interleaved (ILP for the LDS pipe).
-__device__ __forceinline__ void aes128_enc2(const RoundKeys& k, uint32_t lb, uint32_t& s0, uint32_t& s1,
-                                            uint32_t& s2, uint32_t& s3, uint32_t& t0, uint32_t& t1,
-                                            uint32_t& t2, uint32_t& t3) {
+// Two independent blocks, rounds interleaved (more LDS requests in flight per wave).
+__device__ __forceinline__ void aes128_enc2(const RoundKeys& k, const RowLanes& L, uint32_t& s0, uint32_t& s1,
+                                            uint32_t& s2, uint32_t& s3, uint32_t& t0, uint32_t& t1, uint32_t& t2,
+                                            uint32_t& t3) {
   s0 ^= k.w[0]; s1 ^= k.w[1]; s2 ^= k.w[2]; s3 ^= k.w[3];
   t0 ^= k.w[0]; t1 ^= k.w[1]; t2 ^= k.w[2]; t3 ^= k.w[3];
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    uint32_t a0 = lds32(tb0(s0) | lb), a1 = lds32(tb1(s1) | lb), a2 = lds32(tb2(s2) | lb), a3 = lds32(tb3(s3) | lb);
-    uint32_t b0 = lds32(tb0(s1) | lb), b1 = lds32(tb1(s2) | lb), b2 = lds32(tb2(s3) | lb), b3 = lds32(tb3(s0) | lb);
-    uint32_t c0 = lds32(tb0(s2) | lb), c1 = lds32(tb1(s3) | lb), c2 = lds32(tb2(s0) | lb), c3 = lds32(tb3(s1) | lb);
-    uint32_t d0 = lds32(tb0(s3) | lb), d1 = lds32(tb1(s0) | lb), d2 = lds32(tb2(s1) | lb), d3 = lds32(tb3(s2) | lb);
-    uint32_t e0 = lds32(tb0(t0) | lb), e1 = lds32(tb1(t1) | lb), e2 = lds32(tb2(t2) | lb), e3 = lds32(tb3(t3) | lb);
-    uint32_t f0 = lds32(tb0(t1) | lb), f1 = lds32(tb1(t2) | lb), f2 = lds32(tb2(t3) | lb), f3 = lds32(tb3(t0) | lb);
-    uint32_t g0 = lds32(tb0(t2) | lb), g1 = lds32(tb1(t3) | lb), g2 = lds32(tb2(t0) | lb), g3 = lds32(tb3(t1) | lb);
-    uint32_t h0 = lds32(tb0(t3) | lb), h1 = lds32(tb1(t0) | lb), h2 = lds32(tb2(t1) | lb), h3 = lds32(tb3(t2) | lb);
-    s0 = xor3(xor3(a0, rotl8(a1), rotl16(a2)), rotl24(a3), k.w[4 * r + 0]);
-    s1 = xor3(xor3(b0, rotl8(b1), rotl16(b2)), rotl24(b3), k.w[4 * r + 1]);
-    s2 = xor3(xor3(c0, rotl8(c1), rotl16(c2)), rotl24(c3), k.w[4 * r + 2]);
-    s3 = xor3(xor3(d0, rotl8(d1), rotl16(d2)), rotl24(d3), k.w[4 * r + 3]);
-    t0 = xor3(xor3(e0, rotl8(e1), rotl16(e2)), rotl24(e3), k.w[4 * r + 0]);
-    t1 = xor3(xor3(f0, rotl8(f1), rotl16(f2)), rotl24(f3), k.w[4 * r + 1]);
-    t2 = xor3(xor3(g0, rotl8(g1), rotl16(g2)), rotl24(g3), k.w[4 * r + 2]);
-    t3 = xor3(xor3(h0, rotl8(h1), rotl16(h2)), rotl24(h3), k.w[4 * r + 3]);
+    enc_round(L, s0, s1, s2, s3, k.w[4 * r], k.w[4 * r + 1], k.w[4 * r + 2], k.w[4 * r + 3]);
+    enc_round(L, t0, t1, t2, t3, k.w[4 * r], k.w[4 * r + 1], k.w[4 * r + 2], k.w[4 * r + 3]);
   }
-  {
-    uint32_t a0 = lds32(tb0(s0) | lb), a1 = lds32(tb1(s1) | lb), a2 = lds32(tb2(s2) | lb), a3 = lds32(tb3(s3) | lb);
-    uint32_t b0 = lds32(tb0(s1) | lb), b1 = lds32(tb1(s2) | lb), b2 = lds32(tb2(s3) | lb), b3 = lds32(tb3(s0) | lb);
-    uint32_t c0 = lds32(tb0(s2) | lb), c1 = lds32(tb1(s3) | lb), c2 = lds32(tb2(s0) | lb), c3 = lds32(tb3(s1) | lb);
-    uint32_t d0 = lds32(tb0(s3) | lb), d1 = lds32(tb1(s0) | lb), d2 = lds32(tb2(s1) | lb), d3 = lds32(tb3(s2) | lb);
-    s0 = xor3(__builtin_amdgcn_perm(a1, a0, 0x0c0c0501u), __builtin_amdgcn_perm(a3, a2, 0x05010c0cu), k.w[40]);
-    s1 = xor3(__builtin_amdgcn_perm(b1, b0, 0x0c0c0501u), __builtin_amdgcn_perm(b3, b2, 0x05010c0cu), k.w[41]);
-    s2 = xor3(__builtin_amdgcn_perm(c1, c0, 0x0c0c0501u), __builtin_amdgcn_perm(c3, c2, 0x05010c0cu), k.w[42]);
-    s3 = xor3(__builtin_amdgcn_perm(d1, d0, 0x0c0c0501u), __builtin_amdgcn_perm(d3, d2, 0x05010c0cu), k.w[43]);
-  }
-  {
-    uint32_t a0 = lds32(tb0(t0) | lb), a1 = lds32(tb1(t1) | lb), a2 = lds32(tb2(t2) | lb), a3 = lds32(tb3(t3) | lb);
-    uint32_t b0 = lds32(tb0(t1) | lb), b1 = lds32(tb1(t2) | lb), b2 = lds32(tb2(t3) | lb), b3 = lds32(tb3(t0) | lb);
-    uint32_t c0 = lds32(tb0(t2) | lb), c1 = lds32(tb1(t3) | lb), c2 = lds32(tb2(t0) | lb), c3 = lds32(tb3(t1) | lb);
-    uint32_t d0 = lds32(tb0(t3) | lb), d1 = lds32(tb1(t0) | lb), d2 = lds32(tb2(t1) | lb), d3 = lds32(tb3(t2) | lb);
-    t0 = xor3(__builtin_amdgcn_perm(a1, a0, 0x0c0c0501u), __builtin_amdgcn_perm(a3, a2, 0x05010c0cu), k.w[40]);
-    t1 = xor3(__builtin_amdgcn_perm(b1, b0, 0x0c0c0501u), __builtin_amdgcn_perm(b3, b2, 0x05010c0cu), k.w[41]);
-    t2 = xor3(__builtin_amdgcn_perm(c1, c0, 0x0c0c0501u), __builtin_amdgcn_perm(c3, c2, 0x05010c0cu), k.w[42]);
-    t3 = xor3(__builtin_amdgcn_perm(d1, d0, 0x0c0c0501u), __builtin_amdgcn_perm(d3, d2, 0x05010c0cu), k.w[43]);
-  }
+  enc_last(L, s0, s1, s2, s3, k.w[40], k.w[41], k.w[42], k.w[43]);
+  enc_last(L, t0, t1, t2, t3, k.w[40], k.w[41], k.w[42], k.w[43]);
 }
 
-// AES-128 decryption (FIPS-197 §5.3.5 equivalent inverse cipher).  Td0 replicated x32 at
-// dbase, the inverse S-box (as words, Si[x] in byte 0) replicated x32 at sbase; both bases
-// multiples of 32 KiB; lane term ld = (lane & 31) * 4 is OR-ed in by the caller's dbase|ld.
-__device__ __forceinline__ void aes128_dec(const RoundKeys& k, uint32_t ldd, uint32_t lds_, uint32_t& s0,
+// AES-128 decryption (FIPS-197 §5.3.5 equivalent inverse cipher) with the Td0/Td1 row image
+// (lanes LD) and the inverse S-box image at lbs = sbase | (lane&31)*4 for the last round.
+__device__ __forceinline__ uint32_t sb0(uint32_t w) { return (w << 7) & 0x7f80u; }
+__device__ __forceinline__ uint32_t sb1(uint32_t w) { return (w >> 1) & 0x7f80u; }
+__device__ __forceinline__ uint32_t sb2(uint32_t w) { return (w >> 9) & 0x7f80u; }
+__device__ __forceinline__ uint32_t sb3(uint32_t w) { return (w >> 17) & 0x7f80u; }
+
+__device__ __forceinline__ void aes128_dec(const RoundKeys& k, const RowLanes& LD, uint32_t lbs, uint32_t& s0,
                                            uint32_t& s1, uint32_t& s2, uint32_t& s3) {
   s0 ^= k.w[0];
   s1 ^= k.w[1];
@@ -145,44 +138,81 @@ __device__ __forceinline__ void aes128_dec(const RoundKeys& k, uint32_t ldd, uin
   s3 ^= k.w[3];
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    uint32_t a0 = lds32(tb0(s0) | ldd), a1 = lds32(tb1(s3) | ldd), a2 = lds32(tb2(s2) | ldd), a3 = lds32(tb3(s1) | ldd);
-    uint32_t b0 = lds32(tb0(s1) | ldd), b1 = lds32(tb1(s0) | ldd), b2 = lds32(tb2(s3) | ldd), b3 = lds32(tb3(s2) | ldd);
-    uint32_t c0 = lds32(tb0(s2) | ldd), c1 = lds32(tb1(s1) | ldd), c2 = lds32(tb2(s0) | ldd), c3 = lds32(tb3(s3) | ldd);
-    uint32_t d0 = lds32(tb0(s3) | ldd), d1 = lds32(tb1(s2) | ldd), d2 = lds32(tb2(s1) | ldd), d3 = lds32(tb3(s0) | ldd);
-    s0 = xor3(xor3(a0, rotl8(a1), rotl16(a2)), rotl24(a3), k.w[4 * r + 0]);
-    s1 = xor3(xor3(b0, rotl8(b1), rotl16(b2)), rotl24(b3), k.w[4 * r + 1]);
-    s2 = xor3(xor3(c0, rotl8(c1), rotl16(c2)), rotl24(c3), k.w[4 * r + 2]);
-    s3 = xor3(xor3(d0, rotl8(d1), rotl16(d2)), rotl24(d3), k.w[4 * r + 3]);
+    // InvShiftRows: output column c takes row r from column c - r
+    const uint32_t a0 = lds32(ra<0>(s0, LD.l0)), a1 = lds32(ra<1>(s3, LD.l1)), a2 = lds32(ra<2>(s2, LD.l0)), a3 = lds32(ra<3>(s1, LD.l1));
+    const uint32_t b0 = lds32(ra<0>(s1, LD.l0)), b1 = lds32(ra<1>(s0, LD.l1)), b2 = lds32(ra<2>(s3, LD.l0)), b3 = lds32(ra<3>(s2, LD.l1));
+    const uint32_t c0 = lds32(ra<0>(s2, LD.l0)), c1 = lds32(ra<1>(s1, LD.l1)), c2 = lds32(ra<2>(s0, LD.l0)), c3 = lds32(ra<3>(s3, LD.l1));
+    const uint32_t d0 = lds32(ra<0>(s3, LD.l0)), d1 = lds32(ra<1>(s2, LD.l1)), d2 = lds32(ra<2>(s1, LD.l0)), d3 = lds32(ra<3>(s0, LD.l1));
+    s0 = xor3(a0, a1, k.w[4 * r + 0]) ^ rotl16(a2 ^ a3);
+    s1 = xor3(b0, b1, k.w[4 * r + 1]) ^ rotl16(b2 ^ b3);
+    s2 = xor3(c0, c1, k.w[4 * r + 2]) ^ rotl16(c2 ^ c3);
+    s3 = xor3(d0, d1, k.w[4 * r + 3]) ^ rotl16(d2 ^ d3);
   }
-  uint32_t a0 = lds32(tb0(s0) | lds_), a1 = lds32(tb1(s3) | lds_), a2 = lds32(tb2(s2) | lds_), a3 = lds32(tb3(s1) | lds_);
-  uint32_t b0 = lds32(tb0(s1) | lds_), b1 = lds32(tb1(s0) | lds_), b2 = lds32(tb2(s3) | lds_), b3 = lds32(tb3(s2) | lds_);
-  uint32_t c0 = lds32(tb0(s2) | lds_), c1 = lds32(tb1(s1) | lds_), c2 = lds32(tb2(s0) | lds_), c3 = lds32(tb3(s3) | lds_);
-  uint32_t d0 = lds32(tb0(s3) | lds_), d1 = lds32(tb1(s2) | lds_), d2 = lds32(tb2(s1) | lds_), d3 = lds32(tb3(s0) | lds_);
-  s0 = xor3(__builtin_amdgcn_perm(a1, a0, 0x0c0c0400u), __builtin_amdgcn_perm(a3, a2, 0x04000c0cu), k.w[40]);
-  s1 = xor3(__builtin_amdgcn_perm(b1, b0, 0x0c0c0400u), __builtin_amdgcn_perm(b3, b2, 0x04000c0cu), k.w[41]);
-  s2 = xor3(__builtin_amdgcn_perm(c1, c0, 0x0c0c0400u), __builtin_amdgcn_perm(c3, c2, 0x04000c0cu), k.w[42]);
-  s3 = xor3(__builtin_amdgcn_perm(d1, d0, 0x0c0c0400u), __builtin_amdgcn_perm(d3, d2, 0x04000c0cu), k.w[43]);
+  const uint32_t a0 = lds32(sb0(s0) | lbs), a1 = lds32(sb1(s3) | lbs), a2 = lds32(sb2(s2) | lbs), a3 = lds32(sb3(s1) | lbs);
+  const uint32_t b0 = lds32(sb0(s1) | lbs), b1 = lds32(sb1(s0) | lbs), b2 = lds32(sb2(s3) | lbs), b3 = lds32(sb3(s2) | lbs);
+  const uint32_t c0 = lds32(sb0(s2) | lbs), c1 = lds32(sb1(s1) | lbs), c2 = lds32(sb2(s0) | lbs), c3 = lds32(sb3(s3) | lbs);
+  const uint32_t d0 = lds32(sb0(s3) | lbs), d1 = lds32(sb1(s2) | lbs), d2 = lds32(sb2(s1) | lbs), d3 = lds32(sb3(s0) | lbs);
+  s0 = xor3(perm(a1, a0, 0x0c0c0400u), perm(a3, a2, 0x04000c0cu), k.w[40]);
+  s1 = xor3(perm(b1, b0, 0x0c0c0400u), perm(b3, b2, 0x04000c0cu), k.w[41]);
+  s2 = xor3(perm(c1, c0, 0x0c0c0400u), perm(c3, c2, 0x04000c0cu), k.w[42]);
+  s3 = xor3(perm(d1, d0, 0x0c0c0400u), perm(d3, d2, 0x04000c0cu), k.w[43]);
 }
 
-// Stage a 256-word table 32-way replicated at `base` (Td0 or the inverse S-box as words).
+// ---------------------------------------------------------------- table staging
+// Row image from a 256-word T0 (Te0 or Td0): row x = [T0[x] x32 | rotl8(T0[x]) x32].
+__device__ __forceinline__ void stage_rows(const uint32_t* __restrict__ t0, uint32_t base) {
+  for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) {
+    const uint32_t v = t0[i >> 6];
+    lds_st32(base + i * 4u, (i & 32u) ? rotl8(v) : v);
+  }
+}
+// 32-way replicated 256-word table with 128-B rows (the inverse S-box image).
 __device__ __forceinline__ void stage_rep32(const uint32_t* __restrict__ t, uint32_t base) {
-  for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x)
-    lds_st32(base + i * 4u, t[i >> 5]);
+  for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x) lds_st32(base + i * 4u, t[i >> 5]);
+}
+__device__ __forceinline__ void stage_copy(const u32x4* __restrict__ src, uint32_t dst_off, uint32_t n16) {
+  for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) lds_st128(dst_off + i * 16u, src[i]);
 }
 
-// X · P with the 64 KiB byte table of P at LDS offset 0 (16 ds_read_b128, XORs paired
-// through v_bitop3).
-__device__ __forceinline__ uint32_t gbyte_off(u32x4 x, int p) {
-  const uint32_t w = x[p >> 2];
-  const int sh = 8 * (p & 3);
-  return ((sh == 0 ? (w << 4) : (w >> (sh - 4))) & 0xff0u) + (uint32_t)p * 4096u;
+// ---------------------------------------------------------------- GHASH
+// Lane constants for the conflict-free byte-table multiply.
+struct GhashLane {
+  uint32_t sh;        // 8 * (k & 3), k = lane & 15
+  bool q1, q2;        // bits of k >> 2
+  uint32_t po[4];     // po[j].byte[i] = ((4j + i + k) & 15) * 16
+};
+__device__ __forceinline__ GhashLane ghash_lane() {
+  GhashLane g;
+  const uint32_t k = threadIdx.x & 15u;
+  g.sh = 8u * (k & 3u);
+  g.q1 = (k >> 2) & 1u;
+  g.q2 = (k >> 3) & 1u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w |= (((4u * j + i + k) & 15u) << 4) << (8 * i);
+    g.po[j] = w;
+  }
+  return g;
 }
-__device__ __forceinline__ u32x4 gmul_byte(u32x4 x) {
+
+// X · P with the [v][p] byte table of P at LDS 0: rotate X by k bytes (X'.byte t = X.byte (t+k)),
+// then 16 conflict-free ds_read_b128 at (X'.byte t) * 256 + ((t + k) & 15) * 16.
+__device__ __forceinline__ u32x4 gmul_byte(u32x4 x, const GhashLane& g) {
+  const uint32_t y0 = __builtin_amdgcn_alignbit(x[1], x[0], g.sh);
+  const uint32_t y1 = __builtin_amdgcn_alignbit(x[2], x[1], g.sh);
+  const uint32_t y2 = __builtin_amdgcn_alignbit(x[3], x[2], g.sh);
+  const uint32_t y3 = __builtin_amdgcn_alignbit(x[0], x[3], g.sh);
+  const uint32_t z0 = g.q1 ? y1 : y0, z1 = g.q1 ? y2 : y1, z2 = g.q1 ? y3 : y2, z3 = g.q1 ? y0 : y3;
+  const uint32_t w[4] = {g.q2 ? z2 : z0, g.q2 ? z3 : z1, g.q2 ? z0 : z2, g.q2 ? z1 : z3};
   u32x4 r = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int p = 0; p < 16; p += 2) {
-    const u32x4 e1 = lds128(gbyte_off(x, p));
-    const u32x4 e2 = lds128(gbyte_off(x, p + 1));
+  for (int t = 0; t < 16; t += 2) {
+    const uint32_t sa = 0x0c0c0000u | ((4u + (t & 3)) << 8) | (uint32_t)(t & 3);
+    const uint32_t sb = 0x0c0c0000u | ((4u + ((t + 1) & 3)) << 8) | (uint32_t)((t + 1) & 3);
+    const u32x4 e1 = lds128(perm(w[t >> 2], g.po[t >> 2], sa));
+    const u32x4 e2 = lds128(perm(w[(t + 1) >> 2], g.po[(t + 1) >> 2], sb));
 #pragma unroll
     for (int c = 0; c < 4; ++c) r[c] = xor3(r[c], e1[c], e2[c]);
   }
@@ -240,17 +270,6 @@ __device__ __forceinline__ u32x4 shfl_xor4(u32x4 v, int m) {
   return r;
 }
 
-// Stage the 32-way replicated Te0 image at LDS offset tbase (all threads of the block help).
-__device__ __forceinline__ void stage_te0(const uint32_t* __restrict__ te0, uint32_t tbase) {
-  for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x)
-    lds_st32(tbase + i * 4u, te0[i >> 5]);
-}
-
-__device__ __forceinline__ void stage_copy(const u32x4* __restrict__ src, uint32_t dst_off, uint32_t n16) {
-  for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x)
-    lds_st128(dst_off + i * 16u, src[i]);
-}
-
 // Partial-block helpers (bytes [0, n) of a 16-byte block at an arbitrary address).
 __device__ __forceinline__ u32x4 load_partial(const uint8_t* p, uint32_t n) {
   uint32_t b[16];
@@ -262,9 +281,7 @@ __device__ __forceinline__ u32x4 load_partial(const uint8_t* p, uint32_t n) {
   return r;
 }
 __device__ __forceinline__ void store_partial(uint8_t* p, u32x4 v, uint32_t n) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if ((uint32_t)i < n) p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
+  for (uint32_t i = 0; i < n; ++i) p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
 }
 __device__ __forceinline__ u32x4 mask_bytes(u32x4 v, uint32_t n) {  // keep bytes [0, n)
 #pragma unroll

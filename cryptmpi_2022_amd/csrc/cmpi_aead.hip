@@ -133,6 +133,7 @@ struct GcmPlan {
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
+std::atomic<int> g_gcm_unroll{2};  // AES blocks in flight per lane in the GCM kernel (1 or 2)
 
 GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   GcmPlan p{};
@@ -192,7 +193,7 @@ int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
 
 template <int L, bool DEC>
 int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
-  auto fn = cmpi::dev::gcm_batch_kernel<L, DEC>;
+  auto fn = g_gcm_unroll.load() == 1 ? cmpi::dev::gcm_batch_kernel<L, DEC, 1> : cmpi::dev::gcm_batch_kernel<L, DEC, 2>;
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), device, lds);
   if (rc) return rc;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
@@ -232,7 +233,6 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.G = p.G;
   a.r0 = p.r0;
   a.ngroups = (uint32_t)(nrec * p.nseg);
-  a.tbase = (p.L > 1) ? 98304u : 65536u;
   a.htab = reinterpret_cast<const u32x4*>(c->dt->htab[p.L == 1 ? 0 : (p.L == 2 ? 1 : 2)]);
   a.ntab = reinterpret_cast<const u32x4*>(c->dt->ntab[0]);
   a.te0 = c->dt->te0;
@@ -252,7 +252,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     int rc = get_pw(c, p.G, p.nseg, &pw);
     if (rc) return rc;
   }
-  const size_t lds = (size_t)a.tbase + 32768;
+  const size_t lds = cmpi::dev::gcm_lds_bytes(p.L);
   const uint64_t want = ((uint64_t)a.ngroups * p.L + kGcmThreads - 1) / kGcmThreads;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->ncu));
   int rc;
@@ -337,7 +337,11 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   oa.te0 = c->dt->te0;
   oa.off0 = d_off0;
   oa.rk = c->rk;
-  hipLaunchKernelGGL(cmpi::dev::ocb_offset_kernel, dim3((uint32_t)((nrec + 255) / 256)), dim3(256), 32768, st, oa);
+  {
+    int rc0 = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ocb_offset_kernel), c->device, 65536);
+    if (rc0) return rc0;
+  }
+  hipLaunchKernelGGL(cmpi::dev::ocb_offset_kernel, dim3((uint32_t)((nrec + 255) / 256)), dim3(256), 65536, st, oa);
   HIP_TRY(hipGetLastError());
 
   cmpi::dev::OcbArgs a{};
@@ -362,13 +366,13 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.rk = c->rk;
   a.drk = c->drk;
   const size_t lds = DEC ? cmpi::dev::kOcbLdsOpen : cmpi::dev::kOcbLdsSeal;
-  const uint32_t per_cu = DEC ? 2u : 4u;  // LDS-limited 512-thread blocks per CU
+  const uint32_t per_cu = DEC ? 1u : 2u;  // LDS-limited 1024-thread blocks per CU
   auto fn = cmpi::dev::ocb_batch_kernel<DEC>;
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds);
   if (rc) return rc;
   const uint64_t waves = a.nitems;
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + 7) / 8, (uint64_t)c->ncu * per_cu));
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(512), lds, st, a);
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + 15) / 16, (uint64_t)c->ncu * per_cu));
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(1024), lds, st, a);
   HIP_TRY(hipGetLastError());
 
   cmpi::dev::OcbFinalArgs f{};
@@ -388,6 +392,10 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   f.off0 = d_off0;
   f.status = st_arr;
   f.rk = c->rk;
+  {
+    int rc1 = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ocb_final_kernel<DEC>), c->device, cmpi::dev::kOcbLdsSeal);
+    if (rc1) return rc1;
+  }
   hipLaunchKernelGGL(cmpi::dev::ocb_final_kernel<DEC>, dim3((uint32_t)((nrec + 255) / 256)), dim3(256),
                      cmpi::dev::kOcbLdsSeal, st, f);
   HIP_TRY(hipGetLastError());
@@ -464,11 +472,13 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   a.ctr_lo = cmpi::be64(ctr + 8);
   a.te0 = c->dt->te0;
   a.rk = c->rk;
-  const uint64_t blocks = (a.nblk + 511) / 512;  // 2 blocks per thread per pass
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 4));
+  const uint64_t blocks = (a.nblk + 2047) / 2048;  // 2 blocks per thread per pass
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 2));
   hipStream_t st = (hipStream_t)stream;
-  if (in) hipLaunchKernelGGL(cmpi::dev::ctr_kernel<true>, dim3(grid), dim3(256), 32768, st, a);
-  else hipLaunchKernelGGL(cmpi::dev::ctr_kernel<false>, dim3(grid), dim3(256), 32768, st, a);
+  auto fn = in ? cmpi::dev::ctr_kernel<true> : cmpi::dev::ctr_kernel<false>;
+  int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, 65536);
+  if (rc) return rc;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(1024), 65536, st, a);
   HIP_TRY(hipGetLastError());
   return CMPI_OK;
 }
@@ -590,6 +600,8 @@ void cmpi_ctx_free(cmpi_ctx* c) {
 }
 
 int cmpi_ctx_device(const cmpi_ctx* c) { return c ? c->device : -1; }
+
+void cmpi_debug_set_gcm_unroll(int u) { g_gcm_unroll.store(u == 1 ? 1 : 2); }
 
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
   g_force_L.store(lanes_per_record == 1 || lanes_per_record == 2 || lanes_per_record == 4 ? lanes_per_record : 0);
@@ -724,8 +736,10 @@ int cmpi_ecb_encrypt(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t 
   a.nblk = nblocks;
   a.te0 = c->dt->te0;
   a.rk = c->rk;
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 255) / 256, (uint64_t)c->ncu * 4));
-  hipLaunchKernelGGL(cmpi::dev::ecb_kernel, dim3(grid), dim3(256), 32768, (hipStream_t)stream, a);
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 1023) / 1024, (uint64_t)c->ncu * 2));
+  int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ecb_kernel), c->device, 65536);
+  if (rc) return rc;
+  hipLaunchKernelGGL(cmpi::dev::ecb_kernel, dim3(grid), dim3(1024), 65536, (hipStream_t)stream, a);
   HIP_TRY(hipGetLastError());
   return CMPI_OK;
 }

@@ -49,11 +49,12 @@ __device__ __forceinline__ void ctr_emit(const CtrArgs& a, uint64_t j, u32x4 ks)
   }
 }
 
+// LDS: AES row image @0 (64 KiB) -> two 1024-thread blocks per CU.
 template <bool XOR_IN>
-__global__ __launch_bounds__(256) void ctr_kernel(CtrArgs a) {
-  stage_te0(a.te0, 0u);
+__global__ __launch_bounds__(1024) void ctr_kernel(CtrArgs a) {
+  stage_rows(a.te0, 0u);
   __syncthreads();
-  const uint32_t lb = (threadIdx.x & 31u) << 2;
+  const RowLanes lb = row_lanes(0u);
   const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
   uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; j + nthreads < a.nblk; j += 2u * nthreads) {
@@ -81,10 +82,10 @@ struct EcbArgs {
   RoundKeys rk;
 };
 
-__global__ __launch_bounds__(256) void ecb_kernel(EcbArgs a) {
-  stage_te0(a.te0, 0u);
+__global__ __launch_bounds__(1024) void ecb_kernel(EcbArgs a) {
+  stage_rows(a.te0, 0u);
   __syncthreads();
-  const uint32_t lb = (threadIdx.x & 31u) << 2;
+  const RowLanes lb = row_lanes(0u);
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.nblk; j += (uint64_t)gridDim.x * blockDim.x) {
     const u32x4 v = *reinterpret_cast<const u32x4a*>(a.in + 16u * j);
     uint32_t s0 = v[0], s1 = v[1], s2 = v[2], s3 = v[3];

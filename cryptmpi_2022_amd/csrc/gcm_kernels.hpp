@@ -32,8 +32,7 @@ struct GcmArgs {
   uint32_t G;       // X-blocks per segment (all but the first)
   uint32_t r0;      // X-blocks in the first segment
   uint32_t ngroups; // nrec * nseg
-  uint32_t tbase;   // LDS offset of the replicated Te0
-  const u32x4* htab;   // byte table of H^L (global), 4096 entries
+  const u32x4* htab;   // [v][p] byte table of H^L (global), 4096 entries
   const u32x4* ntab;   // nibble tables of H^1..H^L (global), L*512 entries (L > 1)
   const uint32_t* te0; // Te0 (global), 256 words
   u32x4* partial;      // nrec*nseg segment partials (nseg > 1)
@@ -45,16 +44,23 @@ struct GcmArgs {
 __device__ __forceinline__ u32x4 ld_blk(const uint8_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
 __device__ __forceinline__ void st_blk(uint8_t* p, u32x4 v) { *reinterpret_cast<u32x4a*>(p) = v; }
 
-template <int L, bool DECRYPT>
+// LDS: GHASH byte table [v][p] @0 (64 KiB), AES row image @64K (64 KiB), nibble tables of
+// H^1..H^L @128K (L x 8 KiB, L > 1).  L = 4 uses the whole 160 KiB of the CU.
+constexpr uint32_t kGcmRows = 65536u;
+constexpr uint32_t kGcmNib = 131072u;
+__host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return kGcmNib + (L > 1 ? (uint32_t)L * 8192u : 0u); }
+
+// U = AES blocks in flight per lane (1 or 2)
+template <int L, bool DECRYPT, int U>
 __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
-  // ---- stage tables: GHASH byte table @0, nibble tables @64K, Te0 x32 @tbase
   stage_copy(a.htab, 0u, 4096u);
-  if (L > 1) stage_copy(a.ntab, 65536u, (uint32_t)L * 512u);
-  stage_te0(a.te0, a.tbase);
+  stage_rows(a.te0, kGcmRows);
+  if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)L * 512u);
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t lb = a.tbase | ((lane & 31u) << 2);
+  const RowLanes rl = row_lanes(kGcmRows);
+  const GhashLane gl = ghash_lane();
   const uint32_t q = threadIdx.x & (uint32_t)(L - 1);
   const uint32_t nb = a.nb;
   const uint32_t rem = a.len - 16u * (nb ? nb - 1u : 0u);  // bytes in the last data block (1..16)
@@ -103,26 +109,39 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       } else {
         x = lenblk;
       }
-      acc = gmul_byte(acc) ^ x;
+      acc = gmul_byte(acc, gl) ^ x;
     };
 
-    for (uint32_t u = q; u < nslots; u += (uint32_t)L) {
+    uint32_t u = q;
+    if (U == 2) {
+      for (; u + (uint32_t)L < nslots; u += 2u * (uint32_t)L) {
+        const uint32_t ub = u + (uint32_t)L;
+        const uint32_t ca = (u >= nxs) ? 1u : 2u + x0 + u;
+        const uint32_t cb = (ub >= nxs) ? 1u : 2u + x0 + ub;
+        uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = __builtin_bswap32(ca);
+        uint32_t t0 = n0, t1 = n1, t2 = n2, t3 = __builtin_bswap32(cb);
+        aes128_enc2(a.rk, rl, s0, s1, s2, s3, t0, t1, t2, t3);
+        consume(u, u32x4{s0, s1, s2, s3});
+        consume(ub, u32x4{t0, t1, t2, t3});
+      }
+    }
+    for (; u < nslots; u += (uint32_t)L) {
       const uint32_t c = (u >= nxs) ? 1u : 2u + x0 + u;
       uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = __builtin_bswap32(c);
-      aes128_enc(a.rk, lb, s0, s1, s2, s3);
+      aes128_enc(a.rk, rl, s0, s1, s2, s3);
       consume(u, u32x4{s0, s1, s2, s3});
     }
 
     // ---- weight the lane's Horner sum by H^w, w = nxs - (lane's last X slot)
     u32x4 f;
     if (L == 1) {
-      f = gmul_byte(acc);  // L = 1: byte table holds H, w = 1
+      f = gmul_byte(acc, gl);  // L = 1: byte table holds H, w = 1
     } else {
       f = u32x4{0u, 0u, 0u, 0u};
       if (q < nxs) {
         const uint32_t ulast = q + (uint32_t)L * ((nxs - 1u - q) / (uint32_t)L);
         const uint32_t w = nxs - ulast;  // 1..L
-        f = gmul_nib(acc, 65536u + (w - 1u) * 8192u);
+        f = gmul_nib(acc, kGcmNib + (w - 1u) * 8192u);
       }
     }
     if (a.nseg == 1) f ^= ekj0;

@@ -60,8 +60,9 @@ inline Blk gf_pow(const Blk& h, uint64_t e) {
   return r;
 }
 
-// Byte-position table for multiplication by P: tab[p*256 + v] = (block with byte p = v) · P.
-// 16 × 256 × 16 B = 64 KiB.  X·P = XOR_p tab[p*256 + X[p]].
+// Byte-position table for multiplication by P, value-major: tab[v*16 + p] = (block with
+// byte p = v) · P.  16 × 256 × 16 B = 64 KiB.  X·P = XOR_p tab[X[p]*16 + p].  (Value-major so a
+// wave's lanes, each visiting a different position p at a given step, hit distinct LDS slots.)
 inline void build_byte_table(const Blk& P, Blk* tab) {
   for (int p = 0; p < 16; ++p) {
     Blk basis[8];
@@ -75,7 +76,7 @@ inline void build_byte_table(const Blk& P, Blk* tab) {
       for (int k = 0; k < 8; ++k)
         if (v & (1 << k))
           for (int i = 0; i < 16; ++i) acc.b[i] ^= basis[k].b[i];
-      tab[p * 256 + v] = acc;
+      tab[v * 16 + p] = acc;
     }
   }
 }

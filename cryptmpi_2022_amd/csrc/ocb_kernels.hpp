@@ -37,17 +37,17 @@ struct OcbArgs {
   RoundKeys drk;          // equivalent-inverse-cipher keys
 };
 
-// LDS layouts.  seal: Te0 x32 @0, L table @32K (33 KiB).  open: Td0 x32 @0, Si x32 @32K,
-// L table @64K (65 KiB).  offset / final kernels: Te0 @0, L @32K.
-constexpr uint32_t kOcbLSeal = 32768u;
-constexpr uint32_t kOcbLOpen = 65536u;
+// LDS layouts.  seal / offset / final: Te row image @0 (64 KiB), L table @64K.
+// open: Td row image @0 (64 KiB), inverse S-box image @64K (32 KiB), L table @96K.
+constexpr uint32_t kOcbLSeal = 65536u;
+constexpr uint32_t kOcbLOpen = 98304u;
 constexpr uint32_t kOcbLdsSeal = kOcbLSeal + 66u * 16u;
 constexpr uint32_t kOcbLdsOpen = kOcbLOpen + 66u * 16u;
 
 __device__ __forceinline__ u32x4 ocb_l(uint32_t base, uint32_t idx) { return lds128(base + idx * 16u); }
 
 // Offset_0 from the 96-bit nonce (RFC 7253 §4.2): Nonce block = 0^31 || 1 || N.
-__device__ __forceinline__ u32x4 ocb_offset0(const RoundKeys& rk, uint32_t lb, uint32_t n0, uint32_t n1,
+__device__ __forceinline__ u32x4 ocb_offset0(const RoundKeys& rk, const RowLanes& lb, uint32_t n0, uint32_t n1,
                                              uint32_t n2) {
   const uint32_t bottom = (n2 >> 24) & 0x3fu;
   uint32_t s0 = 0x01000000u, s1 = n0, s2 = n1, s3 = n2 & 0xc0ffffffu;
@@ -85,29 +85,29 @@ struct OcbOffsetArgs {
 };
 
 __global__ __launch_bounds__(256) void ocb_offset_kernel(OcbOffsetArgs a) {
-  stage_te0(a.te0, 0u);
+  stage_rows(a.te0, 0u);
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.nrec) return;
   const u32a* np = reinterpret_cast<const u32a*>(a.nonces + (uint64_t)r * a.nonce_stride);
-  a.off0[r] = ocb_offset0(a.rk, (threadIdx.x & 31u) << 2, np[0], np[1], np[2]);
+  a.off0[r] = ocb_offset0(a.rk, row_lanes(0u), np[0], np[1], np[2]);
 }
 
 template <bool DECRYPT>
-__global__ __launch_bounds__(512) void ocb_batch_kernel(OcbArgs a) {
+__global__ __launch_bounds__(1024) void ocb_batch_kernel(OcbArgs a) {
   constexpr uint32_t LB = DECRYPT ? kOcbLOpen : kOcbLSeal;
   if (DECRYPT) {
-    stage_rep32(a.td0, 0u);
-    stage_rep32(a.isb, 32768u);
+    stage_rows(a.td0, 0u);
+    stage_rep32(a.isb, 65536u);
   } else {
-    stage_te0(a.te0, 0u);
+    stage_rows(a.te0, 0u);
   }
   stage_copy(a.ltab, LB, 66u);
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t l32 = (lane & 31u) << 2;
-  const uint32_t lbe = l32, lbd = l32, lbs = 32768u | l32;
+  const RowLanes rl = row_lanes(0u);
+  const uint32_t lbs = 65536u | ((lane & 31u) << 2);
   const uint32_t waves_per_block = blockDim.x >> 6;
   const uint32_t total_waves = gridDim.x * waves_per_block;
   const uint32_t ksteps = a.m / 64u + 1u;  // steps covering i in [0, m]
@@ -135,8 +135,8 @@ __global__ __launch_bounds__(512) void ocb_batch_kernel(OcbArgs a) {
         const u32x4 v = *reinterpret_cast<const u32x4a*>(in_rec + boff);
         u32x4 x = v ^ off;
         uint32_t s0 = x[0], s1 = x[1], s2 = x[2], s3 = x[3];
-        if (DECRYPT) aes128_dec(a.drk, lbd, lbs, s0, s1, s2, s3);
-        else aes128_enc(a.rk, lbe, s0, s1, s2, s3);
+        if (DECRYPT) aes128_dec(a.drk, rl, lbs, s0, s1, s2, s3);
+        else aes128_enc(a.rk, rl, s0, s1, s2, s3);
         const u32x4 y = u32x4{s0, s1, s2, s3} ^ off;
         *reinterpret_cast<u32x4a*>(out_rec + boff) = y;
         csum ^= DECRYPT ? y : v;
@@ -166,12 +166,12 @@ struct OcbFinalArgs {
 // One thread per record: checksum reduction, trailing partial block, tag.
 template <bool DECRYPT>
 __global__ __launch_bounds__(256) void ocb_final_kernel(OcbFinalArgs a) {
-  stage_te0(a.te0, 0u);
+  stage_rows(a.te0, 0u);
   stage_copy(a.ltab, kOcbLSeal, 66u);
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.nrec) return;
-  const uint32_t lb = (threadIdx.x & 31u) << 2;
+  const RowLanes lb = row_lanes(0u);
   const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
   uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
   u32x4 csum = {0u, 0u, 0u, 0u};
