@@ -123,6 +123,48 @@ __device__ __forceinline__ void aes128_enc2(const RoundKeys& k, const RowLanes& 
   enc_last(L, t0, t1, t2, t3, k.w[40], k.w[41], k.w[42], k.w[43]);
 }
 
+// ---------------------------------------------------------------- counter-mode caching
+// For counter blocks that differ only in their last byte (block byte 15 = byte 3 of word 3),
+// round 1 has one varying lookup (Te1[b3(t3)] into column 0) and round 2 one varying lookup per
+// column (the four bytes of round-1 column 0).  Everything else is a per-window constant:
+// rounds 1+2 cost 5 lookups instead of 32 (Bernstein & Schwabe, "New AES software speed
+// records", counter-mode caching).  A window = 256 consecutive counters sharing bytes 0..14.
+struct CtrCache {
+  uint32_t k0;              // round-1 column 0 without its varying term
+  uint32_t q0, q1, q2, q3;  // round-2 columns without the term fed by round-1 column 0
+};
+
+// w0..w3: any counter block of the window (byte 3 of w3 is ignored).
+__device__ __forceinline__ void ctr_cache_fill(const RoundKeys& k, const RowLanes& L, uint32_t w0, uint32_t w1,
+                                               uint32_t w2, uint32_t w3, CtrCache& c) {
+  const uint32_t t0 = w0 ^ k.w[0], t1 = w1 ^ k.w[1], t2 = w2 ^ k.w[2], t3 = w3 ^ k.w[3];
+  c.k0 = xor3(lds32(ra<0>(t0, L.l0)), lds32(ra<1>(t1, L.l1)), k.w[4]) ^ rotl16(lds32(ra<2>(t2, L.l0)));
+  const uint32_t r1 = xor3(lds32(ra<0>(t1, L.l0)), lds32(ra<1>(t2, L.l1)), k.w[5]) ^
+                      rotl16(lds32(ra<2>(t3, L.l0)) ^ lds32(ra<3>(t0, L.l1)));
+  const uint32_t r2 = xor3(lds32(ra<0>(t2, L.l0)), lds32(ra<1>(t3, L.l1)), k.w[6]) ^
+                      rotl16(lds32(ra<2>(t0, L.l0)) ^ lds32(ra<3>(t1, L.l1)));
+  const uint32_t r3 = xor3(lds32(ra<0>(t3, L.l0)), lds32(ra<1>(t0, L.l1)), k.w[7]) ^
+                      rotl16(lds32(ra<2>(t1, L.l0)) ^ lds32(ra<3>(t2, L.l1)));
+  c.q0 = xor3(lds32(ra<1>(r1, L.l1)), k.w[8], rotl16(lds32(ra<2>(r2, L.l0)) ^ lds32(ra<3>(r3, L.l1))));
+  c.q1 = xor3(lds32(ra<0>(r1, L.l0)), lds32(ra<1>(r2, L.l1)), k.w[9]) ^ rotl16(lds32(ra<2>(r3, L.l0)));
+  c.q2 = xor3(lds32(ra<0>(r2, L.l0)), lds32(ra<1>(r3, L.l1)), k.w[10]) ^ rotl16(lds32(ra<3>(r1, L.l1)));
+  c.q3 = xor3(lds32(ra<0>(r3, L.l0)), k.w[11], rotl16(lds32(ra<2>(r1, L.l0)) ^ lds32(ra<3>(r2, L.l1))));
+}
+
+// E_K(counter block) for a block of the cached window; w3 = its last word.
+__device__ __forceinline__ void aes128_enc_ctr(const RoundKeys& k, const RowLanes& L, const CtrCache& c, uint32_t w3,
+                                               uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+  const uint32_t t3 = w3 ^ k.w[3];
+  const uint32_t r0 = c.k0 ^ rotl16(lds32(ra<3>(t3, L.l1)));
+  s0 = c.q0 ^ lds32(ra<0>(r0, L.l0));
+  s3 = c.q3 ^ lds32(ra<1>(r0, L.l1));
+  s2 = c.q2 ^ rotl16(lds32(ra<2>(r0, L.l0)));
+  s1 = c.q1 ^ rotl16(lds32(ra<3>(r0, L.l1)));
+#pragma unroll
+  for (int r = 3; r < 10; ++r) enc_round(L, s0, s1, s2, s3, k.w[4 * r], k.w[4 * r + 1], k.w[4 * r + 2], k.w[4 * r + 3]);
+  enc_last(L, s0, s1, s2, s3, k.w[40], k.w[41], k.w[42], k.w[43]);
+}
+
 // AES-128 decryption (FIPS-197 §5.3.5 equivalent inverse cipher) with the Td0/Td1 row image
 // (lanes LD) and the inverse S-box image at lbs = sbase | (lane&31)*4 for the last round.
 __device__ __forceinline__ uint32_t sb0(uint32_t w) { return (w << 7) & 0x7f80u; }

@@ -133,7 +133,7 @@ struct GcmPlan {
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
-std::atomic<int> g_gcm_unroll{2};  // AES blocks in flight per lane in the GCM kernel (1 or 2)
+std::atomic<int> g_ctr_lds{65536};  // LDS requested by the CTR kernel (occupancy experiments)
 
 GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   GcmPlan p{};
@@ -193,7 +193,7 @@ int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
 
 template <int L, bool DEC>
 int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
-  auto fn = g_gcm_unroll.load() == 1 ? cmpi::dev::gcm_batch_kernel<L, DEC, 1> : cmpi::dev::gcm_batch_kernel<L, DEC, 2>;
+  auto fn = cmpi::dev::gcm_batch_kernel<L, DEC>;
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), device, lds);
   if (rc) return rc;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
@@ -472,13 +472,14 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   a.ctr_lo = cmpi::be64(ctr + 8);
   a.te0 = c->dt->te0;
   a.rk = c->rk;
-  const uint64_t blocks = (a.nblk + 2047) / 2048;  // 2 blocks per thread per pass
+  const uint64_t blocks = (a.nblk + 1023) / 1024;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 2));
   hipStream_t st = (hipStream_t)stream;
   auto fn = in ? cmpi::dev::ctr_kernel<true> : cmpi::dev::ctr_kernel<false>;
-  int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, 65536);
+  const int lds = g_ctr_lds.load();
+  int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds);
   if (rc) return rc;
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(1024), 65536, st, a);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(1024), lds, st, a);
   HIP_TRY(hipGetLastError());
   return CMPI_OK;
 }
@@ -601,7 +602,9 @@ void cmpi_ctx_free(cmpi_ctx* c) {
 
 int cmpi_ctx_device(const cmpi_ctx* c) { return c ? c->device : -1; }
 
-void cmpi_debug_set_gcm_unroll(int u) { g_gcm_unroll.store(u == 1 ? 1 : 2); }
+void cmpi_debug_set_ctr_lds(int lds_bytes) {
+  g_ctr_lds.store(lds_bytes >= 65536 && lds_bytes <= 163840 ? lds_bytes : 65536);
+}
 
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
   g_force_L.store(lanes_per_record == 1 || lanes_per_record == 2 || lanes_per_record == 4 ? lanes_per_record : 0);

@@ -50,27 +50,38 @@ __device__ __forceinline__ void ctr_emit(const CtrArgs& a, uint64_t j, u32x4 ks)
 }
 
 // LDS: AES row image @0 (64 KiB) -> two 1024-thread blocks per CU.
+// Wave step = 64 consecutive counters in one 64-aligned counter window (lane = offset), so each
+// step's counters share bytes 0..14 and the round-1/2 cache is refilled wave-uniformly once
+// every 4 steps.  Each wave owns a contiguous run of steps; loads/stores are 1 KiB coalesced.
 template <bool XOR_IN>
 __global__ __launch_bounds__(1024) void ctr_kernel(CtrArgs a) {
   stage_rows(a.te0, 0u);
   __syncthreads();
-  const RowLanes lb = row_lanes(0u);
-  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; j + nthreads < a.nblk; j += 2u * nthreads) {
-    const uint64_t jb = j + nthreads;
-    uint32_t s0, s1, s2, s3, t0, t1, t2, t3;
-    ctr_words(a.ctr_hi, a.ctr_lo, j, s0, s1, s2, s3);
-    ctr_words(a.ctr_hi, a.ctr_lo, jb, t0, t1, t2, t3);
-    aes128_enc2(a.rk, lb, s0, s1, s2, s3, t0, t1, t2, t3);
-    ctr_emit<XOR_IN>(a, j, u32x4{s0, s1, s2, s3});
-    ctr_emit<XOR_IN>(a, jb, u32x4{t0, t1, t2, t3});
-  }
-  if (j < a.nblk) {
+  const RowLanes rl = row_lanes(0u);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t phase = a.ctr_lo & 63u;        // counter(v) = (ctr & ~63) + v, j = v - phase
+  const uint64_t lo_base = a.ctr_lo & ~63ull;
+  const uint64_t nsteps = (a.nblk + phase + 63u) / 64u;
+  const uint64_t wpb = blockDim.x >> 6;
+  const uint64_t waves = (uint64_t)gridDim.x * wpb;
+  const uint64_t wave = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+  const uint64_t per = (nsteps + waves - 1u) / waves;
+  const uint64_t st0 = wave * per;
+  const uint64_t st1 = min(st0 + per, nsteps);
+  CtrCache cc;
+  uint64_t win = ~0ull;
+  for (uint64_t st = st0; st < st1; ++st) {
+    const uint64_t v = st * 64u + lane;
+    uint32_t w0, w1, w2, w3;
+    ctr_words(a.ctr_hi, lo_base, v, w0, w1, w2, w3);
+    const uint64_t key = ((a.ctr_lo & 0xc0u) + st * 64u) >> 8;  // wave-uniform
+    if (key != win) {
+      ctr_cache_fill(a.rk, rl, w0, w1, w2, w3, cc);
+      win = key;
+    }
     uint32_t s0, s1, s2, s3;
-    ctr_words(a.ctr_hi, a.ctr_lo, j, s0, s1, s2, s3);
-    aes128_enc(a.rk, lb, s0, s1, s2, s3);
-    ctr_emit<XOR_IN>(a, j, u32x4{s0, s1, s2, s3});
+    aes128_enc_ctr(a.rk, rl, cc, w3, s0, s1, s2, s3);
+    if (v >= phase && v - phase < a.nblk) ctr_emit<XOR_IN>(a, v - phase, u32x4{s0, s1, s2, s3});
   }
 }
 

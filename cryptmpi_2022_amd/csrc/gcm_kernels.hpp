@@ -50,8 +50,7 @@ constexpr uint32_t kGcmRows = 65536u;
 constexpr uint32_t kGcmNib = 131072u;
 __host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return kGcmNib + (L > 1 ? (uint32_t)L * 8192u : 0u); }
 
-// U = AES blocks in flight per lane (1 or 2)
-template <int L, bool DECRYPT, int U>
+template <int L, bool DECRYPT>
 __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   stage_copy(a.htab, 0u, 4096u);
   stage_rows(a.te0, kGcmRows);
@@ -112,23 +111,18 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       acc = gmul_byte(acc, gl) ^ x;
     };
 
-    uint32_t u = q;
-    if (U == 2) {
-      for (; u + (uint32_t)L < nslots; u += 2u * (uint32_t)L) {
-        const uint32_t ub = u + (uint32_t)L;
-        const uint32_t ca = (u >= nxs) ? 1u : 2u + x0 + u;
-        const uint32_t cb = (ub >= nxs) ? 1u : 2u + x0 + ub;
-        uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = __builtin_bswap32(ca);
-        uint32_t t0 = n0, t1 = n1, t2 = n2, t3 = __builtin_bswap32(cb);
-        aes128_enc2(a.rk, rl, s0, s1, s2, s3, t0, t1, t2, t3);
-        consume(u, u32x4{s0, s1, s2, s3});
-        consume(ub, u32x4{t0, t1, t2, t3});
+    // counter blocks of a record share the nonce; windows of 256 counters share bytes 0..14
+    CtrCache cc;
+    uint32_t cc_win = 0xffffffffu;
+    for (uint32_t u = q; u < nslots; u += (uint32_t)L) {
+      const uint32_t ctr = (u >= nxs) ? 1u : 2u + x0 + u;  // J0 = nonce || 1, block j = nonce || 2 + j
+      const uint32_t w3 = __builtin_bswap32(ctr);
+      if ((ctr >> 8) != cc_win) {
+        ctr_cache_fill(a.rk, rl, n0, n1, n2, w3, cc);
+        cc_win = ctr >> 8;
       }
-    }
-    for (; u < nslots; u += (uint32_t)L) {
-      const uint32_t c = (u >= nxs) ? 1u : 2u + x0 + u;
-      uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = __builtin_bswap32(c);
-      aes128_enc(a.rk, rl, s0, s1, s2, s3);
+      uint32_t s0, s1, s2, s3;
+      aes128_enc_ctr(a.rk, rl, cc, w3, s0, s1, s2, s3);
       consume(u, u32x4{s0, s1, s2, s3});
     }
 

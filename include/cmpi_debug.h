@@ -17,8 +17,9 @@ extern "C" {
 /* Force GCM lanes-per-record (1, 2 or 4; anything else = automatic) and segments per record
  * (0 = automatic) for every subsequent launch in the process. */
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments);
-/* GCM kernel variant: AES blocks kept in flight per lane (1 or 2; default 2). */
-void cmpi_debug_set_gcm_unroll(int blocks_in_flight);
+/* CTR kernel occupancy experiment: dynamic LDS bytes requested (65536..163840; more than
+ * 80 KiB forces one 1024-thread block per CU). */
+void cmpi_debug_set_ctr_lds(int lds_bytes);
 /* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}. */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);
 
