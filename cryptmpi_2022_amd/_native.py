@@ -68,6 +68,7 @@ _SIGS = {
     "cmpi_ecb_encrypt": ([_P, _P, _P, _S, _P], _I),
     "cmpi_debug_force_plan": ([_I, _U32], None),
     "cmpi_debug_set_ctr_lds": ([_I], None),
+    "cmpi_debug_set_gcm_ablation": ([_I], None),
     "cmpi_debug_gcm_plan": ([_P, _S, _S, _P], _I),
 }
 

@@ -133,7 +133,8 @@ struct GcmPlan {
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
-std::atomic<int> g_ctr_lds{65536};  // LDS requested by the CTR kernel (occupancy experiments)
+std::atomic<int> g_ctr_lds{65536};
+std::atomic<int> g_gcm_ablation{0};  // timing ablation of the L=4 seal kernel (tools/ablate.py)  // LDS requested by the CTR kernel (occupancy experiments)
 
 GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   GcmPlan p{};
@@ -194,6 +195,14 @@ int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
 template <int L, bool DEC>
 int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
   auto fn = cmpi::dev::gcm_batch_kernel<L, DEC>;
+  if constexpr (L == 4 && !DEC) {
+    switch (g_gcm_ablation.load()) {
+      case 1: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 1>; break;
+      case 2: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 2>; break;
+      case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 3>; break;
+      default: break;
+    }
+  }
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), device, lds);
   if (rc) return rc;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
@@ -601,6 +610,8 @@ void cmpi_ctx_free(cmpi_ctx* c) {
 }
 
 int cmpi_ctx_device(const cmpi_ctx* c) { return c ? c->device : -1; }
+
+void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 3); }
 
 void cmpi_debug_set_ctr_lds(int lds_bytes) {
   g_ctr_lds.store(lds_bytes >= 65536 && lds_bytes <= 163840 ? lds_bytes : 65536);

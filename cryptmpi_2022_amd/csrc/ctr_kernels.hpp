@@ -33,15 +33,23 @@ __device__ __forceinline__ void ctr_words(uint64_t hi, uint64_t lo, uint64_t j, 
   w3 = __builtin_bswap32((uint32_t)l2);
 }
 
+// full input block j (prefetched before the AES of its step), zeros otherwise
 template <bool XOR_IN>
-__device__ __forceinline__ void ctr_emit(const CtrArgs& a, uint64_t j, u32x4 ks) {
+__device__ __forceinline__ u32x4 ctr_load(const CtrArgs& a, uint64_t v, uint64_t phase) {
+  if (!XOR_IN || v < phase) return u32x4{0u, 0u, 0u, 0u};
+  const uint64_t off = (v - phase) * 16u;
+  if (off + 16u > a.n) return u32x4{0u, 0u, 0u, 0u};
+  return *reinterpret_cast<const u32x4a*>(a.in + off);
+}
+
+template <bool XOR_IN>
+__device__ __forceinline__ void ctr_emit(const CtrArgs& a, uint64_t j, u32x4 ks, u32x4 v) {
   const uint64_t off = j * 16u;
   if (!XOR_IN) {
     *reinterpret_cast<u32x4a*>(a.out + off) = ks;
     return;
   }
   if (off + 16u <= a.n) {
-    const u32x4 v = *reinterpret_cast<const u32x4a*>(a.in + off);
     *reinterpret_cast<u32x4a*>(a.out + off) = v ^ ks;
   } else {
     const uint32_t rem = (uint32_t)(a.n - off);
@@ -54,7 +62,7 @@ __device__ __forceinline__ void ctr_emit(const CtrArgs& a, uint64_t j, u32x4 ks)
 // step's counters share bytes 0..14 and the round-1/2 cache is refilled wave-uniformly once
 // every 4 steps.  Each wave owns a contiguous run of steps; loads/stores are 1 KiB coalesced.
 template <bool XOR_IN>
-__global__ __launch_bounds__(1024) void ctr_kernel(CtrArgs a) {
+__global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
   stage_rows(a.te0, 0u);
   __syncthreads();
   const RowLanes rl = row_lanes(0u);
@@ -70,8 +78,10 @@ __global__ __launch_bounds__(1024) void ctr_kernel(CtrArgs a) {
   const uint64_t st1 = min(st0 + per, nsteps);
   CtrCache cc;
   uint64_t win = ~0ull;
+  u32x4 in_cur = ctr_load<XOR_IN>(a, st0 * 64u + lane, phase);
   for (uint64_t st = st0; st < st1; ++st) {
     const uint64_t v = st * 64u + lane;
+    const u32x4 in_next = (st + 1u < st1) ? ctr_load<XOR_IN>(a, v + 64u, phase) : u32x4{0u, 0u, 0u, 0u};
     uint32_t w0, w1, w2, w3;
     ctr_words(a.ctr_hi, lo_base, v, w0, w1, w2, w3);
     const uint64_t key = ((a.ctr_lo & 0xc0u) + st * 64u) >> 8;  // wave-uniform
@@ -81,7 +91,8 @@ __global__ __launch_bounds__(1024) void ctr_kernel(CtrArgs a) {
     }
     uint32_t s0, s1, s2, s3;
     aes128_enc_ctr(a.rk, rl, cc, w3, s0, s1, s2, s3);
-    if (v >= phase && v - phase < a.nblk) ctr_emit<XOR_IN>(a, v - phase, u32x4{s0, s1, s2, s3});
+    if (v >= phase && v - phase < a.nblk) ctr_emit<XOR_IN>(a, v - phase, u32x4{s0, s1, s2, s3}, in_cur);
+    in_cur = in_next;
   }
 }
 

@@ -50,7 +50,9 @@ constexpr uint32_t kGcmRows = 65536u;
 constexpr uint32_t kGcmNib = 131072u;
 __host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return kGcmNib + (L > 1 ? (uint32_t)L * 8192u : 0u); }
 
-template <int L, bool DECRYPT>
+// ABL (timing ablation, wrong results): 0 = full kernel, 1 = GHASH multiply skipped,
+// 2 = AES skipped (keystream = counter block), 3 = both skipped.
+template <int L, bool DECRYPT, int ABL = 0>
 __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   stage_copy(a.htab, 0u, 4096u);
   stage_rows(a.te0, kGcmRows);
@@ -82,9 +84,14 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
 
     u32x4 acc = {0u, 0u, 0u, 0u};
     u32x4 ekj0 = {0u, 0u, 0u, 0u};
-
-    // process slot u's AES output `ks`; returns the X block (or J0 handled)
-    auto consume = [&](uint32_t u, u32x4 ks) {
+    // Input blocks are software-prefetched two slots ahead: loads and stores share vmcnt, so a
+    // load consumed right after issue would also wait for the previous slot's store to retire.
+    auto full_blk = [&](uint32_t u) { return u < nxs && x0 + u < nb && (x0 + u + 1u < nb || rem == 16u); };
+    auto prefetch = [&](uint32_t u) -> u32x4 {
+      return full_blk(u) ? ld_blk(in_rec + 16u * (x0 + u)) : u32x4{0u, 0u, 0u, 0u};
+    };
+    // slot u with keystream ks and its prefetched input block v
+    auto consume = [&](uint32_t u, u32x4 ks, u32x4 v) {
       if (u >= nxs) {  // J0 slot
         ekj0 = ks;
         return;
@@ -92,38 +99,46 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       const uint32_t j = x0 + u;
       u32x4 x;
       if (j < nb) {
-        const uint8_t* ip = in_rec + 16u * j;
         uint8_t* op = out_rec + 16u * j;
-        if (j + 1u < nb || rem == 16u) {
-          const u32x4 v = ld_blk(ip);
+        if (full_blk(u)) {
           const u32x4 o = v ^ ks;
           st_blk(op, o);
           x = DECRYPT ? v : o;
         } else {
-          const u32x4 v = load_partial(ip, rem);
-          const u32x4 o = mask_bytes(v ^ ks, rem);
+          const u32x4 p = load_partial(in_rec + 16u * j, rem);
+          const u32x4 o = mask_bytes(p ^ ks, rem);
           store_partial(op, o, rem);
-          x = DECRYPT ? v : o;
+          x = DECRYPT ? p : o;
         }
       } else {
         x = lenblk;
       }
-      acc = gmul_byte(acc, gl) ^ x;
+      if (ABL & 1) acc ^= x;
+      else acc = gmul_byte(acc, gl) ^ x;
     };
 
     // counter blocks of a record share the nonce; windows of 256 counters share bytes 0..14
     CtrCache cc;
     uint32_t cc_win = 0xffffffffu;
-    for (uint32_t u = q; u < nslots; u += (uint32_t)L) {
+    auto keystream = [&](uint32_t u) -> u32x4 {
       const uint32_t ctr = (u >= nxs) ? 1u : 2u + x0 + u;  // J0 = nonce || 1, block j = nonce || 2 + j
       const uint32_t w3 = __builtin_bswap32(ctr);
-      if ((ctr >> 8) != cc_win) {
+      if (!(ABL & 2) && (ctr >> 8) != cc_win) {
         ctr_cache_fill(a.rk, rl, n0, n1, n2, w3, cc);
         cc_win = ctr >> 8;
       }
-      uint32_t s0, s1, s2, s3;
-      aes128_enc_ctr(a.rk, rl, cc, w3, s0, s1, s2, s3);
-      consume(u, u32x4{s0, s1, s2, s3});
+      uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = w3;
+      if (!(ABL & 2)) aes128_enc_ctr(a.rk, rl, cc, w3, s0, s1, s2, s3);
+      return u32x4{s0, s1, s2, s3};
+    };
+    const uint32_t Lu = (uint32_t)L;
+    u32x4 va = prefetch(q), vb = prefetch(q + Lu);
+    for (uint32_t u = q; u < nslots; u += 2u * Lu) {
+      const u32x4 na = prefetch(u + 2u * Lu), nb2 = prefetch(u + 3u * Lu);
+      consume(u, keystream(u), va);
+      if (u + Lu < nslots) consume(u + Lu, keystream(u + Lu), vb);
+      va = na;
+      vb = nb2;
     }
 
     // ---- weight the lane's Horner sum by H^w, w = nxs - (lane's last X slot)

@@ -93,8 +93,9 @@ __global__ __launch_bounds__(256) void ocb_offset_kernel(OcbOffsetArgs a) {
   a.off0[r] = ocb_offset0(a.rk, row_lanes(0u), np[0], np[1], np[2]);
 }
 
+// seal: 65 KiB LDS -> two 1024-thread blocks per CU if VGPRs <= 64 (8 waves per SIMD)
 template <bool DECRYPT>
-__global__ __launch_bounds__(1024) void ocb_batch_kernel(OcbArgs a) {
+__global__ __launch_bounds__(1024, DECRYPT ? 4 : 8) void ocb_batch_kernel(OcbArgs a) {
   constexpr uint32_t LB = DECRYPT ? kOcbLOpen : kOcbLSeal;
   if (DECRYPT) {
     stage_rows(a.td0, 0u);
@@ -127,12 +128,20 @@ __global__ __launch_bounds__(1024) void ocb_batch_kernel(OcbArgs a) {
     const u32x4 B = a.off0[r] ^ Dl;
     u32x4 U = ocb_lsum(LB, ((uint64_t)k0 << 6) ^ ((uint64_t)k0 << 5));
     u32x4 csum = {0u, 0u, 0u, 0u};
+    // next step's block is loaded before this step's AES (loads and stores share vmcnt)
+    auto ld = [&](uint32_t k) -> u32x4 {
+      const uint32_t i = 64u * k + lane;
+      return (k < k1 && i >= 1u && i <= a.m) ? *reinterpret_cast<const u32x4a*>(in_rec + 16ull * (i - 1u))
+                                             : u32x4{0u, 0u, 0u, 0u};
+    };
+    u32x4 vcur = ld(k0);
     for (uint32_t k = k0; k < k1; ++k) {
       const uint32_t i = 64u * k + lane;  // RFC block index (1-based)
+      const u32x4 vnext = ld(k + 1u);
       const u32x4 off = B ^ U;
       if (i >= 1u && i <= a.m) {
         const uint64_t boff = 16ull * (i - 1u);
-        const u32x4 v = *reinterpret_cast<const u32x4a*>(in_rec + boff);
+        const u32x4 v = vcur;
         u32x4 x = v ^ off;
         uint32_t s0 = x[0], s1 = x[1], s2 = x[2], s3 = x[3];
         if (DECRYPT) aes128_dec(a.drk, rl, lbs, s0, s1, s2, s3);
@@ -142,6 +151,7 @@ __global__ __launch_bounds__(1024) void ocb_batch_kernel(OcbArgs a) {
         csum ^= DECRYPT ? y : v;
       }
       U ^= L5 ^ ocb_l(LB, 2u + 6u + (uint32_t)__builtin_ctz(k + 1u));
+      vcur = vnext;
     }
 #pragma unroll
     for (int msk = 1; msk < 64; msk <<= 1) csum ^= shfl_xor4(csum, msk);
