@@ -195,11 +195,13 @@ int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
 template <int L, bool DEC>
 int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
   auto fn = cmpi::dev::gcm_batch_kernel<L, DEC>;
-  if constexpr (L == 4 && !DEC) {
+  if constexpr (!DEC) {
     switch (g_gcm_ablation.load()) {
       case 1: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 1>; break;
       case 2: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 2>; break;
       case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 3>; break;
+      case 4: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 4>; break;
+      case 7: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 7>; break;
       default: break;
     }
   }
@@ -611,7 +613,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
 
 int cmpi_ctx_device(const cmpi_ctx* c) { return c ? c->device : -1; }
 
-void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 3); }
+void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 7); }
 
 void cmpi_debug_set_ctr_lds(int lds_bytes) {
   g_ctr_lds.store(lds_bytes >= 65536 && lds_bytes <= 163840 ? lds_bytes : 65536);

@@ -50,8 +50,9 @@ constexpr uint32_t kGcmRows = 65536u;
 constexpr uint32_t kGcmNib = 131072u;
 __host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return kGcmNib + (L > 1 ? (uint32_t)L * 8192u : 0u); }
 
-// ABL (timing ablation, wrong results): 0 = full kernel, 1 = GHASH multiply skipped,
-// 2 = AES skipped (keystream = counter block), 3 = both skipped.
+// ABL (timing ablation, wrong results): bit 0 = GHASH multiply skipped, bit 1 = AES skipped
+// (keystream = counter block), bit 2 = record data addressed as one coalesced stream per wave
+// (same bytes moved, dense layouts only).
 template <int L, bool DECRYPT, int ABL = 0>
 __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   stage_copy(a.htab, 0u, 4096u);
@@ -87,7 +88,14 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
     // Input blocks are software-prefetched two slots ahead: loads and stores share vmcnt, so a
     // load consumed right after issue would also wait for the previous slot's store to retire.
     auto full_blk = [&](uint32_t u) { return u < nxs && x0 + u < nb && (x0 + u + 1u < nb || rem == 16u); };
+    const uint64_t wave_gid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t ablk_total = (uint64_t)a.nrec * nb;
+    auto abl_off = [&](uint32_t u) -> uint64_t {  // ABL & 4: coalesced stand-in for block (r, x0+u)
+      const uint64_t p = (wave_gid * ((nslots + L - 1) / L) + u / (uint32_t)L) * 64u + lane;
+      return 16u * (p % ablk_total);
+    };
     auto prefetch = [&](uint32_t u) -> u32x4 {
+      if (ABL & 4) return full_blk(u) ? ld_blk(a.in + abl_off(u)) : u32x4{0u, 0u, 0u, 0u};
       return full_blk(u) ? ld_blk(in_rec + 16u * (x0 + u)) : u32x4{0u, 0u, 0u, 0u};
     };
     // slot u with keystream ks and its prefetched input block v
@@ -99,7 +107,7 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       const uint32_t j = x0 + u;
       u32x4 x;
       if (j < nb) {
-        uint8_t* op = out_rec + 16u * j;
+        uint8_t* op = (ABL & 4) ? a.out + abl_off(u) : out_rec + 16u * j;
         if (full_blk(u)) {
           const u32x4 o = v ^ ks;
           st_blk(op, o);

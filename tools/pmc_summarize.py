@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (gpurun_out/pmc_<wl>/p*/run_counter_collection.csv) into
+profiles/pmc_<wl>.json: per-kernel average counters and, for the dominant seal kernel, the HBM
+traffic per launch corrected as MI355X_MICROARCH.md §HBM prescribes:
+  FETCH_SIZE (KiB) reports 1/2 of a 16-B-per-lane streaming read on gfx950 -> x2;
+  WRITE_SIZE (KiB) is exact for 16-B-per-lane streaming stores.
+Usage: tools/pmc_summarize.py <workload> <pmc dir> <kernel substring>"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+wl, d, ksub = sys.argv[1], sys.argv[2], sys.argv[3]
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+durs = collections.defaultdict(list)
+for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        name = r["Kernel_Name"]
+        if "cmpi::dev" not in name:
+            continue
+        short = name.split("(")[0].replace("void cmpi::dev::", "")
+        agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        durs[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+out = {"workload": wl, "source": d, "kernels": {}}
+for k, cs in agg.items():
+    avg = {c: sum(v) / len(v) for c, v in cs.items()}
+    dur = sum(durs[k]) / len(durs[k])
+    e = {"counters_avg": {c: round(v, 1) for c, v in avg.items()}, "avg_duration_us": round(dur * 1e6, 2)}
+    if "GRBM_GUI_ACTIVE" in avg:
+        e["clock_GHz"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9, 3)
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        e["hbm_read_bytes"] = int(avg["FETCH_SIZE"] * 2 * 1024)
+        e["hbm_write_bytes"] = int(avg["WRITE_SIZE"] * 1024)
+        e["traffic_bytes_per_launch"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
+    out["kernels"][k] = e
+dom = [k for k in out["kernels"] if ksub in k]
+if dom:
+    out["dominant_kernel"] = dom[0]
+    out["traffic_bytes_per_launch"] = out["kernels"][dom[0]].get("traffic_bytes_per_launch")
+os.makedirs("profiles", exist_ok=True)
+with open(os.path.join("profiles", f"pmc_{wl}.json"), "w") as f:
+    json.dump(out, f, indent=1)
+print(json.dumps({k: v.get("traffic_bytes_per_launch") for k, v in out["kernels"].items()}, indent=1))
