@@ -69,6 +69,7 @@ _SIGS = {
     "cmpi_debug_force_plan": ([_I, _U32], None),
     "cmpi_debug_set_ctr_lds": ([_I], None),
     "cmpi_debug_set_gcm_ablation": ([_I], None),
+    "cmpi_debug_set_sched": ([_I], None),
     "cmpi_debug_gcm_plan": ([_P, _S, _S, _P], _I),
 }
 

@@ -303,6 +303,20 @@ __device__ __forceinline__ u32x4 gmul_generic(u32x4 x, u32x4 y) {
   return z;
 }
 
+// Wave-issue fairness.  The SQ arbitrates VALU/LDS issue by priority, then age, so waves of a
+// workgroup that carry EQUAL work finish far apart (measured with tools/probe/lds_probe.hip:
+// lifetimes 190K..418K cycles for identical AES loops) and the CU idles through the tail.
+// Rotating each wave's priority every loop iteration ((t + wave) mod 4, t wave-uniform)
+// spreads issue fairly: -11 % time on the probe at one 1024-thread block per CU.
+__device__ __forceinline__ void rotate_prio(uint32_t t) {
+  switch ((__builtin_amdgcn_readfirstlane(t) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) & 3u) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+}
+
 __device__ __forceinline__ u32x4 shfl_xor4(u32x4 v, int m) {
   u32x4 r;
   r[0] = __shfl_xor((int)v[0], m);

@@ -134,6 +134,7 @@ struct GcmPlan {
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
 std::atomic<int> g_ctr_lds{65536};
+std::atomic<int> g_sched{7};         // wave-priority rotation: bit 0 GCM, bit 1 CTR, bit 2 OCB
 std::atomic<int> g_gcm_ablation{0};  // timing ablation of the L=4 seal kernel (tools/ablate.py)  // LDS requested by the CTR kernel (occupancy experiments)
 
 GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
@@ -249,6 +250,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.te0 = c->dt->te0;
   a.status = status;
   a.rk = c->rk;
+  a.sched = (uint32_t)g_sched.load();
   const u32x4* pw = nullptr;
   if (p.nseg > 1) {
     uint8_t* ws = (uint8_t*)workspace;
@@ -375,6 +377,7 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.off0 = d_off0;
   a.partial = d_part;
   a.rk = c->rk;
+  a.sched = (uint32_t)g_sched.load();
   a.drk = c->drk;
   const size_t lds = DEC ? cmpi::dev::kOcbLdsOpen : cmpi::dev::kOcbLdsSeal;
   const uint32_t per_cu = DEC ? 1u : 2u;  // LDS-limited 1024-thread blocks per CU
@@ -483,6 +486,7 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   a.ctr_lo = cmpi::be64(ctr + 8);
   a.te0 = c->dt->te0;
   a.rk = c->rk;
+  a.sched = (uint32_t)g_sched.load();
   const uint64_t blocks = (a.nblk + 1023) / 1024;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 2));
   hipStream_t st = (hipStream_t)stream;
@@ -613,6 +617,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
 
 int cmpi_ctx_device(const cmpi_ctx* c) { return c ? c->device : -1; }
 
+void cmpi_debug_set_sched(int mode) { g_sched.store(mode & 7); }
 void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 7); }
 
 void cmpi_debug_set_ctr_lds(int lds_bytes) {

@@ -20,6 +20,7 @@ struct CtrArgs {
   uint64_t nblk;      // ceil(n/16)
   uint64_t ctr_hi, ctr_lo;  // counter block as two big-endian halves
   const uint32_t* te0;
+  uint32_t sched;  // bit 1: rotate wave priority per step
   RoundKeys rk;
 };
 
@@ -80,6 +81,7 @@ __global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
   uint64_t win = ~0ull;
   u32x4 in_cur = ctr_load<XOR_IN>(a, st0 * 64u + lane, phase);
   for (uint64_t st = st0; st < st1; ++st) {
+    if (a.sched & 2u) rotate_prio((uint32_t)st);
     const uint64_t v = st * 64u + lane;
     const u32x4 in_next = (st + 1u < st1) ? ctr_load<XOR_IN>(a, v + 64u, phase) : u32x4{0u, 0u, 0u, 0u};
     uint32_t w0, w1, w2, w3;

@@ -38,6 +38,7 @@ struct GcmArgs {
   u32x4* partial;      // nrec*nseg segment partials (nseg > 1)
   u32x4* ekj0;         // nrec E_K(J0) (nseg > 1)
   int32_t* status;     // open: per-record result (may be null)
+  uint32_t sched;      // bit 0: rotate wave priority per slot pair (rotate_prio)
   RoundKeys rk;
 };
 
@@ -141,7 +142,9 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
     };
     const uint32_t Lu = (uint32_t)L;
     u32x4 va = prefetch(q), vb = prefetch(q + Lu);
+    uint32_t it = 0;
     for (uint32_t u = q; u < nslots; u += 2u * Lu) {
+      if (a.sched & 1u) rotate_prio(it++);
       const u32x4 na = prefetch(u + 2u * Lu), nb2 = prefetch(u + 3u * Lu);
       consume(u, keystream(u), va);
       if (u + Lu < nslots) consume(u + Lu, keystream(u + Lu), vb);

@@ -33,6 +33,7 @@ struct OcbArgs {
   const u32x4* ltab;      // [0] = L_*, [1] = L_$, [2 + i] = L_i (i < 64)
   const u32x4* off0;      // per-record Offset_0 (ocb_offset_kernel)
   u32x4* partial;         // nitems checksum partials
+  uint32_t sched;         // bit 2: rotate wave priority per step
   RoundKeys rk;           // encryption keys
   RoundKeys drk;          // equivalent-inverse-cipher keys
 };
@@ -136,6 +137,7 @@ __global__ __launch_bounds__(1024, DECRYPT ? 4 : 8) void ocb_batch_kernel(OcbArg
     };
     u32x4 vcur = ld(k0);
     for (uint32_t k = k0; k < k1; ++k) {
+      if (a.sched & 4u) rotate_prio(k);
       const uint32_t i = 64u * k + lane;  // RFC block index (1-based)
       const u32x4 vnext = ld(k + 1u);
       const u32x4 off = B ^ U;
