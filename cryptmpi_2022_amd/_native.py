@@ -47,6 +47,8 @@ _SIGS = {
     "cmpi_device_count": ([], _I),
     "cmpi_ctx_new": ([_I, _P, _S, _S, _I], _P),
     "cmpi_ctx_new_subkey": ([_P, _P], _P),
+    "cmpi_ctx_derive_subkey": ([_P, _P, _P], _P),
+    "cmpi_ctx_rekey_subkey": ([_P, _P, _P, _P], _I),
     "cmpi_ctx_free": ([_P], None),
     "cmpi_ctx_device": ([_P], _I),
     "cmpi_gcm_workspace_size": ([_P, _S, _S], _S),
@@ -66,6 +68,16 @@ _SIGS = {
     "cmpi_iv_count": ([_P, ctypes.c_ulong], None),
     "cmpi_iv_count_out": ([_P, ctypes.c_ulong, _P], None),
     "cmpi_ecb_encrypt": ([_P, _P, _P, _S, _P], _I),
+    "cmpi_602_plan_make": ([_U32, _I, _I, _P], _I),
+    "cmpi_602_plan_from_header": ([_P, _P], _I),
+    "cmpi_602_header": ([_P, _P, _P], _I),
+    "cmpi_602_outer_span": ([_P, _U32, _P, _P, _P, _P], _I),
+    "cmpi_602_seal_outer": ([_P, _P, _P, _P, _P, _U32, _U32, _P], _I),
+    "cmpi_602_seal": ([_P, _P, _P, _P, _P, _P], _I),
+    "cmpi_602_open": ([_P, _P, _P, _P, _P, _P], _I),
+    "cmpi_600_header": ([_U32, ctypes.c_uint8, _P], _I),
+    "cmpi_600_seal": ([_P, _P, _P, _P, _S, _P], _I),
+    "cmpi_600_open": ([_P, _P, _P, _S, _P, _P], _I),
     "cmpi_debug_force_plan": ([_I, _U32], None),
     "cmpi_debug_set_ctr_lds": ([_I], None),
     "cmpi_debug_set_gcm_ablation": ([_I], None),

@@ -87,6 +87,21 @@ class AeadCtx(_Ctx):
             raise N.CmpiError(N.CMPI_EINVAL, N.last_error())
         return cls(b"", "aes-128-gcm", _handle=h)
 
+    @classmethod
+    def derive_subkey(cls, base: "_Ctx", v: bytes, stream=None) -> "AeadCtx":
+        """Stream-ordered 602 sub-key context: K' = AES_K(V), its schedule and GHASH tables are
+        built by one device kernel on `stream` (K' never reaches the host)."""
+        vb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(v))
+        h = N.lib().cmpi_ctx_derive_subkey(base.handle, vb, _stream_ptr(stream))
+        if not h:
+            raise N.CmpiError(N.CMPI_EINVAL, N.last_error())
+        return cls(b"", "aes-128-gcm", _handle=h)
+
+    def rekey_subkey(self, base: "_Ctx", v: bytes, stream=None) -> None:
+        """Re-key this GCM context in place to K' = AES_K(V) on `stream` (no allocation)."""
+        vb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(v))
+        N.check(N.lib().cmpi_ctx_rekey_subkey(self._h, base.handle, vb, _stream_ptr(stream)))
+
     # ------------------------------------------------------------ device-resident batches
     def seal_batch(self, out, inp, nonces, length: int, nrec: int, *, in_stride=None, out_stride=None,
                    nonce_stride=NONCE_LEN, workspace=None, stream=None) -> None:

@@ -24,6 +24,7 @@
 #include "ctr_kernels.hpp"
 #include "gcm_kernels.hpp"
 #include "gf128_host.hpp"
+#include "keysetup_kernels.hpp"
 #include "ocb_kernels.hpp"
 
 using cmpi::Blk;
@@ -70,7 +71,7 @@ struct DevTables {
   uint32_t te0[256];
   uint32_t td0[256];
   uint32_t isb[256];
-  uint32_t pad_[256];            // keeps the GHASH tables 4 KiB aligned
+  uint32_t keys[256];            // [0..43] round keys, [48..51] H (device-keyed contexts read these)
   uint8_t htab[3][kByteTab];     // byte tables for H^1, H^2, H^4
   uint8_t ntab[kNibTables][kNibTab];
   uint8_t ltab[66][16];          // OCB: L_*, L_$, L_0..L_63
@@ -83,6 +84,7 @@ struct cmpi_ctx {
   int device = 0;
   int ncu = 256;
   uint8_t key[16];
+  bool dev_keys = false;  // key, rk, drk and H exist only on the device (derived 602 sub-key)
   cmpi::dev::RoundKeys rk{};
   cmpi::dev::RoundKeys drk{};
   Blk H{};
@@ -163,9 +165,10 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   return p;
 }
 
-size_t gcm_ws_bytes(const GcmPlan& p, size_t nrec) {
+// workspace: partials [nrec][nseg], E_K(J0) [nrec], and for device-keyed contexts H^{kG} [nseg]
+size_t gcm_ws_bytes(const cmpi_ctx* c, const GcmPlan& p, size_t nrec) {
   if (p.nseg <= 1) return 0;
-  return (size_t)nrec * p.nseg * 16 + nrec * 16;
+  return (size_t)nrec * p.nseg * 16 + nrec * 16 + (c->dev_keys ? (size_t)p.nseg * 16 : 0);
 }
 
 int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
@@ -213,18 +216,25 @@ int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size
   return CMPI_OK;
 }
 
+// Where a batch's nonces come from (GcmArgs::nmode): 0 = memory, 1 = "0000000"||wire prefix,
+// 2 = "0000000"||flag||BE32(ctr0 + r) with the prefix written, 3 = fixed 12 bytes.
+struct NonceSpec {
+  uint32_t mode = 0, ctr0 = 0, flag = 0;
+  uint32_t fix[3] = {0, 0, 0};
+};
+
 template <bool DEC>
 int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
               const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status,
-              void* workspace, void* stream) {
+              void* workspace, void* stream, const NonceSpec& ns = NonceSpec()) {
   if (!c) return fail(CMPI_EINVAL, "null ctx");
   if (c->alg != CMPI_AES_128_GCM) return fail(CMPI_EINVAL, "ctx is not AES-128-GCM");
   if (nrec == 0) return CMPI_OK;
-  if (!out || !nonces || (!in && (DEC || len))) return fail(CMPI_EINVAL, "null buffer");
+  if (!out || (!nonces && ns.mode != 3) || (!in && (DEC || len))) return fail(CMPI_EINVAL, "null buffer");
   if (!in) in = out;  // seal of empty records reads nothing
   if (len > 0xFFFFFFF0ull || nrec > 0x7FFFFFFFull) return fail(CMPI_EINVAL, "len/nrec out of range");
   const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
-  if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
+  if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || (ns.mode == 0 && nonce_stride < 12)))
     return fail(CMPI_EINVAL, "stride smaller than record");
   DeviceGuard dg(c->device);
   hipStream_t st = (hipStream_t)stream;
@@ -250,20 +260,32 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.te0 = c->dt->te0;
   a.status = status;
   a.rk = c->rk;
+  a.rkp = c->dev_keys ? c->dt->keys : nullptr;
+  a.nmode = ns.mode;
+  a.nctr0 = ns.ctr0;
+  a.nflag = ns.flag;
+  memcpy(a.nfix, ns.fix, sizeof a.nfix);
   a.sched = (uint32_t)g_sched.load();
   const u32x4* pw = nullptr;
   if (p.nseg > 1) {
     uint8_t* ws = (uint8_t*)workspace;
     if (!ws) {
       std::lock_guard<std::mutex> lk(c->mu);
-      int rc = ensure_buf(&c->scratch, &c->scratch_cap, gcm_ws_bytes(p, nrec));
+      int rc = ensure_buf(&c->scratch, &c->scratch_cap, gcm_ws_bytes(c, p, nrec));
       if (rc) return rc;
       ws = (uint8_t*)c->scratch;
     }
     a.partial = reinterpret_cast<u32x4*>(ws);
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
-    int rc = get_pw(c, p.G, p.nseg, &pw);
-    if (rc) return rc;
+    if (c->dev_keys) {  // H is only on the device: build the combine weights there, in order
+      u32x4* d_pw = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16 + nrec * 16);
+      hipLaunchKernelGGL(cmpi::dev::gcm_powers_kernel, dim3(1), dim3(64), 0, st, c->dt->keys, p.G, p.nseg, d_pw);
+      HIP_TRY(hipGetLastError());
+      pw = d_pw;
+    } else {
+      int rc = get_pw(c, p.G, p.nseg, &pw);
+      if (rc) return rc;
+    }
   }
   const size_t lds = cmpi::dev::gcm_lds_bytes(p.L);
   const uint64_t want = ((uint64_t)a.ngroups * p.L + kGcmThreads - 1) / kGcmThreads;
@@ -474,6 +496,7 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   if (!c) return fail(CMPI_EINVAL, "null ctx");
   if (c->alg != CMPI_AES_128_CTR && c->alg != CMPI_AES_128_GCM && c->alg != CMPI_AES_128_ECB)
     return fail(CMPI_EINVAL, "ctx algorithm cannot run CTR");
+  if (c->dev_keys) return fail(CMPI_EINVAL, "device-derived sub-key context supports GCM only");
   if (!ctr || !out) return fail(CMPI_EINVAL, "null argument");
   if (n == 0) return CMPI_OK;
   DeviceGuard dg(c->device);
@@ -568,6 +591,8 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
   memcpy(ht->te0, cmpi::kAes.te0, sizeof ht->te0);
   memcpy(ht->td0, cmpi::kAes.td0, sizeof ht->td0);
   for (int x = 0; x < 256; ++x) ht->isb[x] = cmpi::kAes.inv_sbox[x];
+  memcpy(ht->keys, c->rk.w, sizeof c->rk.w);
+  memcpy(ht->keys + 48, c->H.b, 16);
   if (alg == CMPI_AES_128_GCM) {
     const Blk H2 = cmpi::gf_mul(c->H, c->H), H3 = cmpi::gf_mul(H2, c->H), H4 = cmpi::gf_mul(H2, H2);
     cmpi::build_byte_table(c->H, reinterpret_cast<Blk*>(ht->htab[0]));
@@ -641,7 +666,7 @@ int cmpi_debug_gcm_plan(const cmpi_ctx* c, size_t len, size_t nrec, uint32_t out
 
 size_t cmpi_gcm_workspace_size(const cmpi_ctx* c, size_t len, size_t nrec) {
   if (!c) return 0;
-  return gcm_ws_bytes(plan_gcm(c, len, nrec), nrec);
+  return gcm_ws_bytes(c, plan_gcm(c, len, nrec), nrec);
 }
 
 int cmpi_gcm_seal_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
@@ -748,6 +773,7 @@ void cmpi_iv_count_out(uint8_t iv[16], unsigned long cter, const uint8_t in[16])
 
 int cmpi_ecb_encrypt(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t nblocks, void* stream) {
   if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (c->dev_keys) return fail(CMPI_EINVAL, "device-derived sub-key context supports GCM only");
   if (!out || !in) return fail(CMPI_EINVAL, "null buffer");
   if (nblocks == 0) return CMPI_OK;
   DeviceGuard dg(c->device);
@@ -765,29 +791,67 @@ int cmpi_ecb_encrypt(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t 
   return CMPI_OK;
 }
 
-cmpi_ctx* cmpi_ctx_new_subkey(const cmpi_ctx* base, const uint8_t v[16]) {
+int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[16], void* stream) {
+  if (!dst || !base || !v) return fail(CMPI_EINVAL, "null argument");
+  if (dst->alg != CMPI_AES_128_GCM) return fail(CMPI_EINVAL, "destination ctx is not AES-128-GCM");
+  if (base->dev_keys) return fail(CMPI_EINVAL, "base ctx must hold a host-known master key");
+  if (dst->device != base->device) return fail(CMPI_EINVAL, "contexts on different devices");
+  DeviceGuard dg(dst->device);
+  cmpi::dev::KeysetupArgs a{};
+  a.base = base->rk;
+  memcpy(a.v, v, 16);
+  a.mode = 1;
+  a.te0 = dst->dt->te0;
+  a.keys = dst->dt->keys;
+  a.htab = reinterpret_cast<u32x4*>(dst->dt->htab[0]);
+  a.ntab = reinterpret_cast<u32x4*>(dst->dt->ntab[0]);
+  int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_keysetup_kernel), dst->device, cmpi::dev::kKsLds);
+  if (rc) return rc;
+  {
+    std::lock_guard<std::mutex> lk(dst->mu);
+    for (auto& kv : dst->pw) (void)hipFree(kv.second.first);
+    dst->pw.clear();
+    dst->dev_keys = true;
+    memset(dst->key, 0, 16);
+    memset(&dst->rk, 0, sizeof dst->rk);
+    memset(&dst->drk, 0, sizeof dst->drk);
+    memset(&dst->H, 0, sizeof dst->H);
+  }
+  hipLaunchKernelGGL(cmpi::dev::gcm_keysetup_kernel, dim3(1), dim3(256), cmpi::dev::kKsLds, (hipStream_t)stream, a);
+  HIP_TRY(hipGetLastError());
+  return CMPI_OK;
+}
+
+cmpi_ctx* cmpi_ctx_derive_subkey(const cmpi_ctx* base, const uint8_t v[16], void* stream) {
   if (!base || !v) {
     fail(CMPI_EINVAL, "null argument");
     return nullptr;
   }
-  uint8_t kp[16];
-  {
-    DeviceGuard dg(base->device);
-    uint8_t* d = nullptr;
-    if (hipMalloc(&d, 32) != hipSuccess) {
-      fail(CMPI_ENOMEM, "hipMalloc failed");
-      return nullptr;
-    }
-    int rc = CMPI_OK;
-    if (hipMemcpy(d, v, 16, hipMemcpyHostToDevice) != hipSuccess) rc = fail(CMPI_EHIP, "H2D V failed");
-    if (!rc) rc = cmpi_ecb_encrypt(base, d + 16, d, 1, nullptr);
-    if (!rc && hipMemcpy(kp, d + 16, 16, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(CMPI_EHIP, "D2H K' failed");
-    (void)hipFree(d);
-    if (rc) return nullptr;
+  // a GCM context with placeholder keys (all-zero key), re-keyed on the device in stream order
+  static const uint8_t zero[16] = {0};
+  cmpi_ctx* c = cmpi_ctx_new(CMPI_AES_128_GCM, zero, 16, 0, base->device);
+  if (!c) return nullptr;
+  if (cmpi_ctx_rekey_subkey(c, base, v, stream) != CMPI_OK) {
+    std::string e = g_err;
+    cmpi_ctx_free(c);
+    g_err = e;
+    return nullptr;
   }
-  cmpi_ctx* c = cmpi_ctx_new(CMPI_AES_128_GCM, kp, 16, 0, base->device);
-  memset(kp, 0, 16);
+  return c;
+}
+
+cmpi_ctx* cmpi_ctx_new_subkey(const cmpi_ctx* base, const uint8_t v[16]) {
+  cmpi_ctx* c = cmpi_ctx_derive_subkey(base, v, nullptr);
+  if (!c) return nullptr;
+  DeviceGuard dg(c->device);
+  if (hipStreamSynchronize(nullptr) != hipSuccess) {
+    fail(CMPI_EHIP, "key setup failed: %s", hipGetErrorString(hipGetLastError()));
+    cmpi_ctx_free(c);
+    return nullptr;
+  }
   return c;
 }
 
 }  // extern "C"
+
+#include "frame_host.hpp"

@@ -35,12 +35,14 @@ __device__ __forceinline__ void ctr_words(uint64_t hi, uint64_t lo, uint64_t j, 
 }
 
 // full input block j (prefetched before the AES of its step), zeros otherwise
+// Unconditional, clamped: blocks outside [0, nfull) read block 0 (value ignored by ctr_emit);
+// nfull == 0 (no full block at all) reads the Te0 table.
 template <bool XOR_IN>
-__device__ __forceinline__ u32x4 ctr_load(const CtrArgs& a, uint64_t v, uint64_t phase) {
-  if (!XOR_IN || v < phase) return u32x4{0u, 0u, 0u, 0u};
-  const uint64_t off = (v - phase) * 16u;
-  if (off + 16u > a.n) return u32x4{0u, 0u, 0u, 0u};
-  return *reinterpret_cast<const u32x4a*>(a.in + off);
+__device__ __forceinline__ u32x4 ctr_load(const CtrArgs& a, uint64_t v, uint64_t phase, uint64_t nfull) {
+  if (!XOR_IN) return u32x4{0u, 0u, 0u, 0u};
+  const uint64_t j = v - phase;  // wraps for v < phase
+  const uint8_t* base = nfull ? a.in : reinterpret_cast<const uint8_t*>(a.te0);
+  return *reinterpret_cast<const u32x4a*>(base + (j < nfull ? j : 0u) * 16u);
 }
 
 template <bool XOR_IN>
@@ -79,11 +81,12 @@ __global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
   const uint64_t st1 = min(st0 + per, nsteps);
   CtrCache cc;
   uint64_t win = ~0ull;
-  u32x4 in_cur = ctr_load<XOR_IN>(a, st0 * 64u + lane, phase);
+  const uint64_t nfull = a.n / 16u;
+  // the next step's block is loaded right after this step's store: a whole step of AES covers it
+  u32x4 in_cur = ctr_load<XOR_IN>(a, st0 * 64u + lane, phase, nfull);
   for (uint64_t st = st0; st < st1; ++st) {
     if (a.sched & 2u) rotate_prio((uint32_t)st);
     const uint64_t v = st * 64u + lane;
-    const u32x4 in_next = (st + 1u < st1) ? ctr_load<XOR_IN>(a, v + 64u, phase) : u32x4{0u, 0u, 0u, 0u};
     uint32_t w0, w1, w2, w3;
     ctr_words(a.ctr_hi, lo_base, v, w0, w1, w2, w3);
     const uint64_t key = ((a.ctr_lo & 0xc0u) + st * 64u) >> 8;  // wave-uniform
@@ -94,7 +97,7 @@ __global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
     uint32_t s0, s1, s2, s3;
     aes128_enc_ctr(a.rk, rl, cc, w3, s0, s1, s2, s3);
     if (v >= phase && v - phase < a.nblk) ctr_emit<XOR_IN>(a, v - phase, u32x4{s0, s1, s2, s3}, in_cur);
-    in_cur = in_next;
+    in_cur = ctr_load<XOR_IN>(a, v + 64u, phase, nfull);
   }
 }
 

@@ -39,8 +39,31 @@ struct GcmArgs {
   u32x4* ekj0;         // nrec E_K(J0) (nseg > 1)
   int32_t* status;     // open: per-record result (may be null)
   uint32_t sched;      // bit 0: rotate wave priority per slot pair (rotate_prio)
+  const uint32_t* rkp; // device-keyed context: round keys in HBM (keysetup_kernels.hpp), else null
+  // Nonce source (CryptMPI framings, DESIGN.md §"602 framing"):
+  //  0: 12 bytes at nonces + r*nonce_stride
+  //  1: "0000000" || the 5-byte segment prefix at nonces + r*nonce_stride   (602 receiver,
+  //     recv.c:594-609 / :749-764 rebuilds the nonce from the wire)
+  //  2: "0000000" || nflag || BE32(nctr0 + r); seal also writes that 5-byte prefix at
+  //     nonces + r*nonce_stride                                              (602 sender,
+  //     send.c:651-670 / :779-799)
+  //  3: the 12 bytes nfix[] for every record; seal also writes them at nonces + r*nonce_stride
+  //     when nonces != null                                                  (600 sender, one
+  //     RAND_bytes nonce per message, send.c:294-311)
+  uint32_t nmode, nctr0, nflag;
+  uint32_t nfix[3];
   RoundKeys rk;
 };
+
+// Round keys: from the kernel arguments, or (device-derived sub-key contexts) loaded once from
+// HBM at kernel entry — uniform address before any store, so they land in SGPRs like args.
+__device__ __forceinline__ RoundKeys load_round_keys(const RoundKeys& arg, const uint32_t* rkp) {
+  if (!rkp) return arg;
+  RoundKeys k;
+#pragma unroll
+  for (int i = 0; i < 44; ++i) k.w[i] = __builtin_amdgcn_readfirstlane(rkp[i]);
+  return k;
+}
 
 __device__ __forceinline__ u32x4 ld_blk(const uint8_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
 __device__ __forceinline__ void st_blk(uint8_t* p, u32x4 v) { *reinterpret_cast<u32x4a*>(p) = v; }
@@ -61,6 +84,7 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)L * 512u);
   __syncthreads();
 
+  const RoundKeys rk = load_round_keys(a.rk, a.rkp);
   const uint32_t lane = threadIdx.x & 63u;
   const RowLanes rl = row_lanes(kGcmRows);
   const GhashLane gl = ghash_lane();
@@ -81,8 +105,45 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
     const uint32_t nslots = nxs + (s == 0 ? 1u : 0u);  // + the J0 slot
     const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
     uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
-    const u32a* np = reinterpret_cast<const u32a*>(a.nonces + (uint64_t)r * a.nonce_stride);
-    const uint32_t n0 = np[0], n1 = np[1], n2 = np[2];
+    uint32_t n0, n1, n2;
+    {
+      uint8_t* nb8 = const_cast<uint8_t*>(a.nonces) + (uint64_t)r * a.nonce_stride;
+      if (a.nmode == 0u) {
+        const u32a* np = reinterpret_cast<const u32a*>(nb8);
+        n0 = np[0];
+        n1 = np[1];
+        n2 = np[2];
+      } else if (a.nmode == 3u) {
+        n0 = a.nfix[0];
+        n1 = a.nfix[1];
+        n2 = a.nfix[2];
+        if (!DECRYPT && nb8 && s == 0u && q == 0u) {
+          u32a* np = reinterpret_cast<u32a*>(nb8);
+          np[0] = n0;
+          np[1] = n1;
+          np[2] = n2;
+        }
+      } else {
+        uint32_t f, c;
+        if (a.nmode == 1u) {
+          f = nb8[0];
+          c = ((uint32_t)nb8[1] << 24) | ((uint32_t)nb8[2] << 16) | ((uint32_t)nb8[3] << 8) | nb8[4];
+        } else {
+          f = a.nflag;
+          c = a.nctr0 + r;
+          if (!DECRYPT && s == 0u && q == 0u) {
+            nb8[0] = (uint8_t)f;
+            nb8[1] = (uint8_t)(c >> 24);
+            nb8[2] = (uint8_t)(c >> 16);
+            nb8[3] = (uint8_t)(c >> 8);
+            nb8[4] = (uint8_t)c;
+          }
+        }
+        n0 = 0x30303030u;                 // "0000"
+        n1 = 0x00303030u | (f << 24);     // "000" || flag
+        n2 = __builtin_bswap32(c);        // BE32 counter
+      }
+    }
 
     u32x4 acc = {0u, 0u, 0u, 0u};
     u32x4 ekj0 = {0u, 0u, 0u, 0u};
@@ -95,9 +156,15 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       const uint64_t p = (wave_gid * ((nslots + L - 1) / L) + u / (uint32_t)L) * 64u + lane;
       return 16u * (p % ablk_total);
     };
+    // Unconditional load of slot u's block, clamped to a block of this record when slot u has
+    // no full input block (the value is then ignored): no exec-mask branch, no zero-init.
+    // (Records without a full block may have no input at all: read the Te0 table instead.)
+    const bool any_full = nb > 1u || (nb == 1u && rem == 16u);
+    const uint8_t* pf_base = any_full ? in_rec : reinterpret_cast<const uint8_t*>(a.te0);
     auto prefetch = [&](uint32_t u) -> u32x4 {
       if (ABL & 4) return full_blk(u) ? ld_blk(a.in + abl_off(u)) : u32x4{0u, 0u, 0u, 0u};
-      return full_blk(u) ? ld_blk(in_rec + 16u * (x0 + u)) : u32x4{0u, 0u, 0u, 0u};
+      const uint32_t j = full_blk(u) ? x0 + u : 0u;
+      return ld_blk(pf_base + 16u * j);
     };
     // slot u with keystream ks and its prefetched input block v
     auto consume = [&](uint32_t u, u32x4 ks, u32x4 v) {
@@ -133,23 +200,24 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       const uint32_t ctr = (u >= nxs) ? 1u : 2u + x0 + u;  // J0 = nonce || 1, block j = nonce || 2 + j
       const uint32_t w3 = __builtin_bswap32(ctr);
       if (!(ABL & 2) && (ctr >> 8) != cc_win) {
-        ctr_cache_fill(a.rk, rl, n0, n1, n2, w3, cc);
+        ctr_cache_fill(rk, rl, n0, n1, n2, w3, cc);
         cc_win = ctr >> 8;
       }
       uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = w3;
-      if (!(ABL & 2)) aes128_enc_ctr(a.rk, rl, cc, w3, s0, s1, s2, s3);
+      if (!(ABL & 2)) aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
       return u32x4{s0, s1, s2, s3};
     };
     const uint32_t Lu = (uint32_t)L;
+    // Two input buffers: slot u's block is reloaded with slot u+2L's as soon as u is consumed,
+    // so each load has a whole slot of AES in front of its use and no register copies.
     u32x4 va = prefetch(q), vb = prefetch(q + Lu);
     uint32_t it = 0;
     for (uint32_t u = q; u < nslots; u += 2u * Lu) {
       if (a.sched & 1u) rotate_prio(it++);
-      const u32x4 na = prefetch(u + 2u * Lu), nb2 = prefetch(u + 3u * Lu);
       consume(u, keystream(u), va);
+      va = prefetch(u + 2u * Lu);
       if (u + Lu < nslots) consume(u + Lu, keystream(u + Lu), vb);
-      va = na;
-      vb = nb2;
+      vb = prefetch(u + 3u * Lu);
     }
 
     // ---- weight the lane's Horner sum by H^w, w = nxs - (lane's last X slot)

@@ -23,8 +23,9 @@
  *                         cipher.h:158/:174; send.c:985-1008, :1716-1727, :1805-1808
  *   cmpi_ctr_keystream    generateCommonEncMask (E_K(IV+i) over zeros), send.c:1162-1266
  *   cmpi_ecb_encrypt      EVP_EncryptUpdate(ctx_enc, newkey, &len, V, 16), send.c:583
- *   cmpi_ctx_new_subkey   the 602 sub-key: K' = AES-ECB_K(V) then EVP_AEAD_CTX_new(K'),
- *                         send.c:572-600, recv.c:549-576
+ *   cmpi_ctx_new_subkey / derive_subkey / rekey_subkey
+ *                         the 602 sub-key: K' = AES-ECB_K(V) then EVP_AEAD_CTX_new(K'),
+ *                         send.c:572-600, recv.c:549-576 (derived and tabled on the device)
  *   cmpi_iv_count         IV_Count, send.c:1019-1030
  *   cmpi_ocb_seal/open_batch  AES-128-OCB (RFC 7253) — README-only "Naive OCB" (402); no
  *                         reference code exists (OPENSSL_NO_OCB, opensslconf.h:49)
@@ -71,8 +72,17 @@ int cmpi_device_count(void);
  * uploads them to `device` (HIP ordinal).  key_len must be 16.  tag_len 0 or 16.
  * Returns NULL on failure (see cmpi_last_error). */
 cmpi_ctx *cmpi_ctx_new(int alg, const uint8_t *key, size_t key_len, size_t tag_len, int device);
-/* 602 sub-key context: K' = AES-128_K(V) computed by the ECB kernel on the device of
- * `ecb_ctx` (an ECB or GCM context holding K), then a GCM context for K'. */
+/* 602 sub-key (send.c:572-600, recv.c:549-576): a GCM context for K' = AES-128_K(V), where
+ * `base` is any context holding the master key K.  K' never leaves the device: one key-setup
+ * kernel derives K', expands it, computes H = E_K'(0) and builds the GHASH tables.
+ *   cmpi_ctx_derive_subkey  enqueues that kernel on `stream` and returns at once; use the
+ *                           context on the same stream (or after synchronising it).
+ *   cmpi_ctx_rekey_subkey   the same into an existing GCM context `dst` (no allocation: one
+ *                           context per sender/receiver thread reused across messages).
+ *   cmpi_ctx_new_subkey     derive + synchronise (blocking convenience).
+ * A device-keyed context serves the GCM calls only (CTR/ECB on it return CMPI_EINVAL). */
+cmpi_ctx *cmpi_ctx_derive_subkey(const cmpi_ctx *base, const uint8_t v[16], void *stream);
+int cmpi_ctx_rekey_subkey(cmpi_ctx *dst, const cmpi_ctx *base, const uint8_t v[16], void *stream);
 cmpi_ctx *cmpi_ctx_new_subkey(const cmpi_ctx *base, const uint8_t v[16]);
 void cmpi_ctx_free(cmpi_ctx *ctx);
 int cmpi_ctx_device(const cmpi_ctx *ctx);
@@ -84,7 +94,7 @@ int cmpi_ctx_device(const cmpi_ctx *ctx);
  *         nonce  12 bytes                 at nonces + i*nonce_stride.
  *   open: reads  len+16 bytes ct||tag at in, writes len bytes plaintext at out,
  *         status[i] = 1 ok / 0 authentication failure (plaintext zero-filled); status may be NULL.
- * All pointers and strides must be multiples of 4 bytes; len is any value >= 0.  Records must
+ * Pointers and strides may have any byte alignment; len is any value >= 0.  Records must
  * not overlap each other; out may equal in (in-place) but must not partially overlap it.
  * The naive-collective wire layout nonce(12)||ct(n)||tag(16) is expressed as
  *   out = wire + 12, nonces = wire, out_stride = nonce_stride = n + 28.

@@ -171,3 +171,28 @@ def ctr_xor_mt(key: bytes, ctr0: bytes, data: np.ndarray, nthreads: int = 0) -> 
     out = np.empty_like(data)
     lib().orc_ctr128_xor_mt(_buf(key), _buf(ctr0), _ptr(data), _ptr(out), data.nbytes, nthreads)
     return out
+
+
+# ---------------------------------------------------------------- 602 framing (send.c:339-884)
+class _Plan602(ctypes.Structure):
+    _fields_ = [("total", ctypes.c_uint32), ("chop", ctypes.c_uint32), ("outer", ctypes.c_uint32),
+                ("nseg", ctypes.c_uint32), ("mode", ctypes.c_uint8), ("subkey", ctypes.c_uint8),
+                ("wire_bytes", ctypes.c_uint64)]
+
+
+def plan602(n: int, series_threads: int = 8, pending: int = 0) -> dict:
+    p = _Plan602()
+    lib().orc_602_plan(ctypes.c_uint32(n), series_threads, pending, ctypes.byref(p))
+    return {"total": p.total, "chop": p.chop, "outer": p.outer, "nseg": p.nseg, "mode": chr(p.mode),
+            "subkey": bool(p.subkey), "wire_bytes": p.wire_bytes}
+
+
+def seal602(key: bytes, small_key: bytes, pt: bytes, rand16: bytes, series_threads: int = 8, pending: int = 0,
+            wire_fill: int = 0):
+    """(header[25], wire[wire_bytes]) of one 602 message exactly as send.c builds them."""
+    p = _Plan602()
+    lib().orc_602_plan(ctypes.c_uint32(len(pt)), series_threads, pending, ctypes.byref(p))
+    hdr = (ctypes.c_uint8 * 25)()
+    wire = (ctypes.c_uint8 * max(1, p.wire_bytes))(*([wire_fill] * max(1, p.wire_bytes)))
+    lib().orc_602_seal(_buf(key), _buf(small_key), ctypes.byref(p), _buf(rand16), _buf(pt) if pt else None, hdr, wire)
+    return bytes(hdr), bytes(wire)[: p.wire_bytes]

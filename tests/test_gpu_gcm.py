@@ -254,3 +254,48 @@ def test_unaligned_records(n, off, pad):
                    out_stride=in_stride, nonce_stride=n_stride)
     assert (host(st)[:nrec] == 1).all()
     assert np.array_equal(host(back), inbuf)
+
+
+@pytest.mark.parametrize("n,nrec,plan", [(300, 4, None), (4096, 3, (4, 0)), (65536, 2, (4, 5)), (100, 40, (2, 0)),
+                                         (1 << 20, 1, None), (31, 7, (1, 0))])
+def test_derived_subkey_device_keyed(n, nrec, plan):
+    """cmpi_ctx_derive_subkey: K' = AES_K(V), key schedule, H and every GHASH table built by the
+    key-setup kernel on the stream (no host copy of K'); seal/open through every plan shape,
+    incl. multi-segment records whose H^{kG} weights are then also computed on the device."""
+    base = aead.CipherCtx(KEY, "aes-128-ecb")
+    v = splitmix64_bytes(0x60200 + n, 16).tobytes()
+    kprime = oracle.ecb_encrypt(KEY, v)
+    pt = records(13 + n, nrec, n)
+    nonces = np.stack([np.frombuffer(oracle.nonce602(b"1", 7 + i), np.uint8) for i in range(nrec)])
+    try:
+        if plan:
+            aead.force_plan(*plan)
+        sub = aead.AeadCtx.derive_subkey(base, v)
+        want = oracle.gcm_seal_batch(kprime, nonces, pt)
+        assert np.array_equal(gpu_seal(sub, nonces, pt), want)
+        ct = dev(want)
+        d_pt, st = empty(nrec * n), status_buf(nrec)
+        sub.open_batch(d_pt, ct, dev(nonces), n, nrec, status=st)
+        assert (host(st)[:nrec] == 1).all()
+        assert host(d_pt)[: nrec * n].tobytes() == pt.tobytes()
+    finally:
+        aead.force_plan(0, 0)
+
+
+def test_rekey_subkey_reuses_context():
+    """One context re-keyed per message (what a 602 sender thread does per MPI_Send)."""
+    base = aead.AeadCtx(KEY)  # any context holding K serves as the base
+    sub = aead.AeadCtx(bytes(16))
+    pt = records(99, 5, 1000)
+    nonces = np.stack([np.frombuffer(oracle.nonce602(b"0", i), np.uint8) for i in range(5)])
+    for m in range(3):
+        v = splitmix64_bytes(0x777 + m, 16).tobytes()
+        sub.rekey_subkey(base, v)
+        assert np.array_equal(gpu_seal(sub, nonces, pt), oracle.gcm_seal_batch(oracle.ecb_encrypt(KEY, v), nonces, pt)), m
+
+
+def test_device_keyed_ctx_rejects_ctr():
+    base = aead.CipherCtx(KEY, "aes-128-ecb")
+    sub = aead.AeadCtx.derive_subkey(base, bytes(range(16)))
+    rc = aead.N.lib().cmpi_ctr_keystream(sub.handle, None, 1, (aead.ctypes.c_uint8 * 16)(), None)
+    assert rc == aead.N.CMPI_EINVAL
