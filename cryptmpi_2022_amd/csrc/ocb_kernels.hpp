@@ -129,8 +129,8 @@ __global__ __launch_bounds__(1024, DECRYPT ? 4 : 8) void ocb_batch_kernel(OcbArg
     const u32x4 B = a.off0[r] ^ Dl;
     u32x4 U = ocb_lsum(LB, ((uint64_t)k0 << 6) ^ ((uint64_t)k0 << 5));
     u32x4 csum = {0u, 0u, 0u, 0u};
-    // The next step's block is loaded right after this step's store (a whole step of AES covers
-    // it); unconditional and clamped to block 1 (m == 0: the L table) so no branch, no copies.
+    // The next step's block is loaded before this step's AES (loads and stores share vmcnt);
+    // unconditional and clamped to block 1 (m == 0: the L table), so no branch.
     const uint8_t* ld_base = a.m ? in_rec : reinterpret_cast<const uint8_t*>(a.ltab);
     auto ld = [&](uint32_t k) -> u32x4 {
       const uint32_t i = 64u * k + lane;
@@ -140,6 +140,7 @@ __global__ __launch_bounds__(1024, DECRYPT ? 4 : 8) void ocb_batch_kernel(OcbArg
     for (uint32_t k = k0; k < k1; ++k) {
       if (a.sched & 4u) rotate_prio(k);
       const uint32_t i = 64u * k + lane;  // RFC block index (1-based)
+      const u32x4 vnext = ld(k + 1u);
       const u32x4 off = B ^ U;
       if (i >= 1u && i <= a.m) {
         const uint64_t boff = 16ull * (i - 1u);
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(1024, DECRYPT ? 4 : 8) void ocb_batch_kernel(OcbArg
         csum ^= DECRYPT ? y : v;
       }
       U ^= L5 ^ ocb_l(LB, 2u + 6u + (uint32_t)__builtin_ctz(k + 1u));
-      vcur = ld(k + 1u);
+      vcur = vnext;
     }
 #pragma unroll
     for (int msk = 1; msk < 64; msk <<= 1) csum ^= shfl_xor4(csum, msk);
