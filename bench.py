@@ -134,6 +134,38 @@ def time_steps(w: Workload, steps: int, warmup: int, barrier):
     return wall, seal_ms, open_ms
 
 
+def aggregate(wall: float, per_rank_bytes: int, steps: int, pg, device) -> tuple[float, float]:
+    """Whole-job rate: the slowest rank's timed wall clock (MAX over ranks) and the bytes all
+    ranks processed in it, GiB/s (weak scaling: every rank has the same per-rank batch)."""
+    t = torch.tensor([wall], dtype=torch.float64, device=device)
+    ws = 1
+    if pg is not None:
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        ws = pg.get_world_size()
+    wall_max = float(t.item())
+    return wall_max, per_rank_bytes * ws * steps / wall_max / GIB
+
+
+def copy_peak_gbs(device: int, nbytes: int = 1 << 30, reps: int = 10) -> float:
+    """Achievable HBM bandwidth on this box: device-to-device copy of 1 GiB (read + write bytes
+    / time, best of `reps`) — the 'measured copy-kernel peak' of BASELINE.md §3."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", device))
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize(device)
+    best = float("inf")
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src)
+        e1.record()
+        torch.cuda.synchronize(device)
+        best = min(best, e0.elapsed_time(e1) * 1e-3)
+    del src, dst
+    torch.cuda.empty_cache()
+    return 2 * nbytes / best / 1e9
+
+
 def host_path_rate(device: int, n: int = 1024, nrec: int = 65536) -> dict:
     """PCIe-inclusive seal rate: pinned host plaintext -> H2D -> kernel -> D2H -> pinned host."""
     pt = torch.randint(0, 256, (nrec * n,), dtype=torch.uint8).pin_memory()
@@ -307,13 +339,8 @@ def main() -> None:
     w = Workload(args.workload, local, seed=1000 + rank)
     wall, seal_ms, open_ms = time_steps(w, args.steps, args.warmup, barrier)
     ok = w.verify()
-    # max over ranks of the timed wall clock
-    t = torch.tensor([wall], dtype=torch.float64, device=w.dev)
-    if pg is not None:
-        pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    wall_max = float(t.item())
     per_rank_bytes = w.n * w.nrec  # plaintext bytes per step per rank
-    value = per_rank_bytes * ws * args.steps / wall_max / GIB
+    wall_max, value = aggregate(wall, per_rank_bytes, args.steps, pg, w.dev)
     bpl = w.bytes_per_launch()
     kern_ms = seal_ms  # dominant kernel: the seal launch (open is within a few % of it)
     achieved = bpl / (kern_ms * 1e-3) / 1e9
@@ -342,6 +369,13 @@ def main() -> None:
         "verified_round_trip": ok,
     }
     w.free()
+    if rank == 0:
+        try:
+            peak_meas = copy_peak_gbs(local)
+            result["roofline"]["peak_measured"] = round(peak_meas, 1)
+            result["roofline"]["frac_measured"] = round(achieved / peak_meas, 4)
+        except Exception as e:  # report, never hide
+            result["roofline"]["peak_measured"] = {"error": repr(e)}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(args.workload, args.cpu_seconds)
         port = cb.get("port", {})

@@ -68,6 +68,9 @@ _SIGS = {
     "cmpi_iv_count": ([_P, ctypes.c_ulong], None),
     "cmpi_iv_count_out": ([_P, ctypes.c_ulong, _P], None),
     "cmpi_ecb_encrypt": ([_P, _P, _P, _S, _P], _I),
+    "cmpi_gcm_seal_batch_fresh": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
+    "cmpi_naive_seal_blocks": ([_P, _P, _P, _S, _S, _P, _P], _I),
+    "cmpi_naive_open_blocks": ([_P, _P, _P, _S, _S, _P, _P, _P], _I),
     "cmpi_602_plan_make": ([_U32, _I, _I, _P], _I),
     "cmpi_602_plan_from_header": ([_P, _P], _I),
     "cmpi_602_header": ([_P, _P, _P], _I),

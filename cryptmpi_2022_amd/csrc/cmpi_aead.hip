@@ -18,7 +18,10 @@
 #include <string>
 #include <vector>
 
+#include <sys/random.h>
+
 #include "../../include/cmpi_aead.h"
+#include "../../include/cmpi_coll.h"
 #include "../../include/cmpi_debug.h"
 #include "aes_tables.hpp"
 #include "ctr_kernels.hpp"
@@ -85,6 +88,8 @@ struct cmpi_ctx {
   int ncu = 256;
   uint8_t key[16];
   bool dev_keys = false;  // key, rk, drk and H exist only on the device (derived 602 sub-key)
+  cmpi::dev::RoundKeys nrk{};        // nonce DRBG key Kn (OS CSPRNG), cmpi_gcm_seal_batch_fresh
+  std::atomic<uint64_t> nctr{0};     // nonce DRBG counter
   cmpi::dev::RoundKeys rk{};
   cmpi::dev::RoundKeys drk{};
   Blk H{};
@@ -583,6 +588,21 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->ncu = prop.multiProcessorCount;
   cmpi::aes128_expand_words(key, c->rk.w);
   cmpi::aes128_dec_words(c->rk.w, c->drk.w);
+  {
+    uint8_t kn[16];
+    size_t got = 0;
+    while (got < sizeof kn) {
+      const ssize_t r = getrandom(kn + got, sizeof kn - got, 0);
+      if (r <= 0) {
+        fail(CMPI_EHIP, "getrandom failed");
+        delete c;
+        return nullptr;
+      }
+      got += (size_t)r;
+    }
+    cmpi::aes128_expand_words(kn, c->nrk.w);
+    memset(kn, 0, sizeof kn);
+  }
   uint32_t z[4] = {0, 0, 0, 0}, h[4];
   cmpi::aes128_encrypt_words_host(c->rk.w, z, h);  // H = E_K(0^128), L_* for OCB
   memcpy(c->H.b, h, 16);
@@ -681,6 +701,42 @@ int cmpi_gcm_open_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, cons
                         void* workspace, void* stream) {
   return gcm_batch<true>(c, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, status, workspace,
                          stream);
+}
+
+int cmpi_gcm_seal_batch_fresh(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in,
+                              size_t in_stride, uint8_t* nonce_out, size_t nonce_stride, size_t len, size_t nrec,
+                              void* workspace, void* stream) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (nrec == 0) return CMPI_OK;
+  if (!nonce_out) return fail(CMPI_EINVAL, "null nonce_out");
+  if (nrec > 1 && nonce_stride < 12) return fail(CMPI_EINVAL, "nonce_stride < 12");
+  DeviceGuard dg(c->device);
+  cmpi::dev::NonceArgs na{};
+  na.out = nonce_out;
+  na.stride = nonce_stride;
+  na.nrec = nrec;
+  na.base = const_cast<cmpi_ctx*>(c)->nctr.fetch_add(nrec);
+  na.te0 = c->dt->te0;
+  na.rk = c->nrk;
+  int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::nonce_drbg_kernel), c->device, 65536);
+  if (rc) return rc;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nrec + 1023) / 1024, (uint64_t)c->ncu));
+  hipLaunchKernelGGL(cmpi::dev::nonce_drbg_kernel, dim3(grid), dim3(1024), 65536, (hipStream_t)stream, na);
+  HIP_TRY(hipGetLastError());
+  return gcm_batch<false>(c, out, out_stride, in, in_stride, nonce_out, nonce_stride, len, nrec, nullptr, workspace,
+                          stream);
+}
+
+int cmpi_naive_seal_blocks(const cmpi_ctx* c, uint8_t* wire, const uint8_t* in, size_t n, size_t nblk,
+                           void* workspace, void* stream) {
+  if (!wire) return fail(CMPI_EINVAL, "null wire");
+  return cmpi_gcm_seal_batch_fresh(c, wire + 12, n + 28, in, n, wire, n + 28, n, nblk, workspace, stream);
+}
+
+int cmpi_naive_open_blocks(const cmpi_ctx* c, uint8_t* out, const uint8_t* wire, size_t n, size_t nblk,
+                           int32_t* status, void* workspace, void* stream) {
+  if (!wire) return fail(CMPI_EINVAL, "null wire");
+  return gcm_batch<true>(c, out, n, wire + 12, n + 28, wire, n + 28, n, nblk, status, workspace, stream);
 }
 
 int cmpi_gcm_seal_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,

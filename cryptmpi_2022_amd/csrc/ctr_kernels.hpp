@@ -123,3 +123,35 @@ __global__ __launch_bounds__(1024) void ecb_kernel(EcbArgs a) {
 
 }  // namespace dev
 }  // namespace cmpi
+
+namespace cmpi {
+namespace dev {
+
+// Fresh 96-bit nonces for "RAND_bytes(nonce, 12); EVP_AEAD_CTX_seal(...)" call sites
+// (alltoall.c:797, allgather.c:862, gather.c:1533, scatter.c:690, bcast.c:1537, send.c:298):
+// nonce_r = bytes 0..11 of AES_Kn(BE64(base + r) || 0^64), Kn a per-context key drawn from the
+// OS CSPRNG.  AES is a permutation, so the nonces of one context never repeat before 2^64 calls.
+struct NonceArgs {
+  uint8_t* out;
+  uint64_t stride, nrec, base;
+  const uint32_t* te0;
+  RoundKeys rk;
+};
+
+__global__ __launch_bounds__(1024) void nonce_drbg_kernel(NonceArgs a) {
+  stage_rows(a.te0, 0u);
+  __syncthreads();
+  const RowLanes rl = row_lanes(0u);
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.nrec; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = a.base + r;
+    uint32_t s0 = __builtin_bswap32((uint32_t)(c >> 32)), s1 = __builtin_bswap32((uint32_t)c), s2 = 0u, s3 = 0u;
+    aes128_enc(a.rk, rl, s0, s1, s2, s3);
+    u32a* o = reinterpret_cast<u32a*>(a.out + r * a.stride);
+    o[0] = s0;
+    o[1] = s1;
+    o[2] = s2;
+  }
+}
+
+}  // namespace dev
+}  // namespace cmpi
