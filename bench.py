@@ -65,6 +65,8 @@ class Workload:
             self.ctx = aead.CipherCtx(KEY, "aes-128-ctr", device=device)
             self.ct = torch.empty_like(self.pt)
             self.ctr0 = bytes(range(0xF0, 0x100))
+            self.pt_sample = self.pt[: 1 << 24].clone()  # open writes the plaintext back in place
+            self._bind()
             return
         self.ctx = aead.AeadCtx(KEY, "aes-128-gcm" if self.alg == "gcm" else "aes-128-ocb", device=device)
         self.nonces = torch.randint(0, 256, (N * 12,), dtype=torch.uint8, device=self.dev, generator=g)
@@ -73,6 +75,7 @@ class Workload:
         self.status = torch.zeros(N, dtype=torch.int32, device=self.dev)
         ws = self.ctx.workspace_size(n, N)
         self.ws = torch.empty(max(ws, 16), dtype=torch.uint8, device=self.dev) if ws else None
+        self._bind()
 
     # algorithmic HBM bytes per launch: seal/open 2n+28 per record, CTR fused 2n
     def bytes_per_launch(self) -> int:
@@ -80,27 +83,52 @@ class Workload:
             return 2 * self.n
         return self.nrec * (2 * self.n + 28)
 
-    def seal(self):
+    def _bind(self):
+        """Pre-built C-ABI calls (argument tuples converted once): a step enqueues in a few us,
+        so the GPU never idles between launches and the HIP-event kernel times agree with
+        rocprofv3's kernel durations."""
+        from cryptmpi_2022_amd import _native as N
+
+        L, h = N.lib(), self.ctx.handle
+        st = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         if self.alg == "ctr":
-            self.ctx.ctr_xor(self.ct, self.pt, self.n, self.ctr0)
-        else:
-            self.ctx.seal_batch(self.ct, self.pt, self.nonces, self.n, self.nrec, workspace=self.ws)
+            cb = (ctypes.c_uint8 * 16).from_buffer_copy(self.ctr0)
+            self._seal_call = (L.cmpi_ctr_xor, (h, P(self.ct), P(self.pt), self.n, cb, st))
+            self._open_call = (L.cmpi_ctr_xor, (h, P(self.pt), P(self.ct), self.n, cb, st))
+            return
+        n, N_ = self.n, self.nrec
+        seal = L.cmpi_gcm_seal_batch if self.alg == "gcm" else L.cmpi_ocb_seal_batch
+        opn = L.cmpi_gcm_open_batch if self.alg == "gcm" else L.cmpi_ocb_open_batch
+        self._seal_call = (seal, (h, P(self.ct), n + 16, P(self.pt), n, P(self.nonces), 12, n, N_, P(self.ws), st))
+        self._open_call = (opn, (h, P(self.back), n, P(self.ct), n + 16, P(self.nonces), 12, n, N_, P(self.status),
+                                 P(self.ws), st))
+
+    def seal(self):
+        fn, args = self._seal_call
+        rc = fn(*args)
+        if rc:
+            from cryptmpi_2022_amd import _native as N
+
+            N.check(rc)
 
     def open(self):
-        if self.alg == "ctr":
-            self.ctx.ctr_xor(self.back if hasattr(self, "back") else self.pt, self.ct, self.n, self.ctr0)
-        else:
-            self.ctx.open_batch(self.back, self.ct, self.nonces, self.n, self.nrec, status=self.status, workspace=self.ws)
+        fn, args = self._open_call
+        rc = fn(*args)
+        if rc:
+            from cryptmpi_2022_amd import _native as N
+
+            N.check(rc)
 
     def verify(self) -> bool:
         torch.cuda.synchronize(self.dev)
-        if self.alg == "ctr":
-            return True
+        if self.alg == "ctr":  # ct != pt, and decrypting ct in place restored the plaintext
+            return (not torch.equal(self.ct[: 1 << 24], self.pt_sample)) and torch.equal(self.pt[: 1 << 24], self.pt_sample)
         return bool((self.status == 1).all()) and torch.equal(self.back, self.pt)
 
     def free(self):
         self.ctx.close()
-        for a in ("pt", "ct", "back", "nonces", "status", "ws"):
+        for a in ("_seal_call", "_open_call", "pt", "pt_sample", "ct", "back", "nonces", "status", "ws"):
             if hasattr(self, a):
                 delattr(self, a)
         torch.cuda.empty_cache()
@@ -311,8 +339,8 @@ def load_pmc(workload: str):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="gcm1k", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
