@@ -21,14 +21,26 @@ ap.add_argument("--wl", default="gcm1k,gcm4k,ctr1g,ocb1m")
 ap.add_argument("--rounds", type=int, default=7)
 args = ap.parse_args()
 
-libs = []
-for p in args.libs:
-    L = ctypes.CDLL(os.path.abspath(p))
+libs, names = [], []
+for spec in args.libs:  # path[:sched] — the same .so may be loaded twice under different knobs
+    p, _, sched = spec.partition(":")
+    import shutil
+    import tempfile
+
+    path = os.path.abspath(p)
+    if any(os.path.abspath(q.partition(":")[0]) == path for q in args.libs[: len(libs)]):
+        tmp = os.path.join(tempfile.mkdtemp(), os.path.basename(path))  # distinct dlopen instance
+        shutil.copy(path, tmp)
+        path = tmp
+    L = ctypes.CDLL(path)
     for name, (at, rt) in _native._SIGS.items():
         if hasattr(L, name):
             getattr(L, name).argtypes = at
             getattr(L, name).restype = rt
+    if sched:
+        L.cmpi_debug_set_sched(int(sched))
     libs.append(L)
+    names.append(os.path.basename(os.path.dirname(os.path.abspath(p))) + (f"s{sched}" if sched else ""))
 
 dev = torch.device("cuda:0")
 key = bytes(range(16))
@@ -95,7 +107,7 @@ for wl in args.wl.split(","):
     for (i, w), t in times.items():
         t = sorted(t)
         med = t[len(t) // 2]
-        row[f"{os.path.basename(os.path.dirname(args.libs[i]))}_{w}"] = {
+        row[f"{names[i]}_{w}"] = {
             "ms": round(med, 4), "GiBps": round(n * nrec / (med * 1e-3) / 2**30, 1)}
     row["outputs_identical"] = same
     row["round_trip"] = rt

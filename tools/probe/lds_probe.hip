@@ -85,7 +85,9 @@ __device__ __forceinline__ void combine16(const Look16& t, uint32_t& s0, uint32_
 }
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
 
+__device__ __forceinline__ void setprio_dyn(uint32_t p);
 // two blocks per lane, staggered by half a round: B's combine runs while A's lookups are in flight
+template <bool PRIO>
 __global__ __launch_bounds__(1024, 8) void probe_stagger(uint32_t* out, const uint32_t* table, int iters, RoundKeys k,
                                                          unsigned long long* cyc) {
   for (uint32_t i = threadIdx.x; i < 16384u; i += blockDim.x) lds_st32(i * 4u, table[i]);
@@ -95,6 +97,7 @@ __global__ __launch_bounds__(1024, 8) void probe_stagger(uint32_t* out, const ui
   uint32_t a0 = threadIdx.x * 0x9E3779B1u + blockIdx.x, a1 = a0 + 0x1234567u, a2 = a0 + 0x2468ace, a3 = a0 + 0x369d035;
   uint32_t b0 = a0 ^ 0x55555555u, b1 = a1 ^ 0x55555555u, b2 = a2 ^ 0x55555555u, b3 = a3 ^ 0x55555555u;
   for (int it = 0; it < iters; ++it) {
+    if (PRIO) setprio_dyn((uint32_t)it + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     Look16 tb = issue16(L, b0, b1, b2, b3);
     FENCE();
 #pragma unroll
@@ -139,6 +142,19 @@ __global__ __launch_bounds__(1024, 8) void probe_fair(uint32_t* out, const uint3
     if (VARIANT == 0) {
       if (it >= (uint32_t)iters) break;
       setprio_dyn(it + wid);
+      ++it;
+    } else if (VARIANT == 2) {  // progress-based: behind the workgroup average -> higher priority
+      if (it >= (uint32_t)iters) break;
+      typedef __attribute__((address_space(3))) uint32_t lds_u;
+      uint32_t tot = 0;
+      if ((threadIdx.x & 63u) == 0) {
+        __hip_atomic_fetch_add((lds_u*)(size_t)65536u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        tot = *(volatile lds_u*)(size_t)65536u;
+      }
+      tot = __builtin_amdgcn_readfirstlane(tot);
+      const uint32_t avg16 = tot;             // 16 x average iterations done
+      const uint32_t mine16 = (it + 1) * 16u;
+      setprio_dyn(mine16 + 16u <= avg16 ? 3u : (mine16 <= avg16 ? 2u : (mine16 <= avg16 + 16u ? 1u : 0u)));
       ++it;
     } else {
       uint32_t got = 0;
@@ -256,9 +272,11 @@ int main() {
   for (int lds : {163840 - 256, 65536 + 256}) {
     run<0, 1>("real", lds, ncu, out, table, cyc, k);
     run<0, 2>("real", lds, ncu, out, table, cyc, k);
-    run_fn<0, 2>(probe_stagger, "stagger2", lds, ncu, out, table, cyc, k);
+    run_fn<0, 2>(probe_stagger<false>, "stagger2", lds, ncu, out, table, cyc, k);
+    run_fn<0, 2>(probe_stagger<true>, "stagger2_rotprio", lds, ncu, out, table, cyc, k);
     run_fn<0, 1>(probe_fair<0>, "rotprio", lds, ncu, out, table, cyc, k);
     run_fn<0, 1>(probe_fair<1>, "dynamic", lds, ncu, out, table, cyc, k);
+    run_fn<0, 1>(probe_fair<2>, "progress_prio", lds, ncu, out, table, cyc, k);
     run<1, 1>("combine8", lds, ncu, out, table, cyc, k);
     run<1, 2>("combine8", lds, ncu, out, table, cyc, k);
     run<2, 1>("extra16_indep", lds, ncu, out, table, cyc, k);
