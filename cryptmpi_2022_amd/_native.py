@@ -71,6 +71,13 @@ _SIGS = {
     "cmpi_gcm_seal_batch_fresh": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
     "cmpi_naive_seal_blocks": ([_P, _P, _P, _S, _S, _P, _P], _I),
     "cmpi_naive_open_blocks": ([_P, _P, _P, _S, _S, _P, _P, _P], _I),
+    "cmpi_ctr_ring_new": ([_P, _P, _S], _P),
+    "cmpi_ctr_ring_free": ([_P], None),
+    "cmpi_ctr_ring_generate": ([_P, _S, _P], _I),
+    "cmpi_ctr_ring_encrypt": ([_P, _P, _P, _S, _P], _I),
+    "cmpi_ctr_ring_state": ([_P, _P], _I),
+    "cmpi_ctr_mask_decrypt": ([_P, _P, _P, _S, _P, _S, _P, ctypes.c_uint64, _P], _I),
+    "cmpi_xor_bytes": ([_P, _P, _P, _S, _P], _I),
     "cmpi_602_plan_make": ([_U32, _I, _I, _P], _I),
     "cmpi_602_plan_from_header": ([_P, _P], _I),
     "cmpi_602_header": ([_P, _P, _P], _I),

@@ -23,6 +23,7 @@
 #include "../../include/cmpi_aead.h"
 #include "../../include/cmpi_coll.h"
 #include "../../include/cmpi_debug.h"
+#include "../../include/cmpi_ring.h"
 #include "aes_tables.hpp"
 #include "ctr_kernels.hpp"
 #include "gcm_kernels.hpp"
@@ -911,3 +912,4 @@ cmpi_ctx* cmpi_ctx_new_subkey(const cmpi_ctx* base, const uint8_t v[16]) {
 }  // extern "C"
 
 #include "frame_host.hpp"
+#include "ring_host.hpp"

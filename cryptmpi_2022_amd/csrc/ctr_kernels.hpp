@@ -155,3 +155,24 @@ __global__ __launch_bounds__(1024) void nonce_drbg_kernel(NonceArgs a) {
 
 }  // namespace dev
 }  // namespace cmpi
+
+namespace cmpi {
+namespace dev {
+
+// out = a ^ b over n bytes, any byte alignment (mask-ring consumption, send.c:1300-1330 /
+// recv.c:975-1002).  HBM-bound: 16 B per lane per step, grid-stride; the last n % 16 bytes
+// are done bytewise by the lanes that own them.
+__global__ __launch_bounds__(256) void xor_bytes_kernel(uint8_t* out, const uint8_t* a, const uint8_t* b, uint64_t n) {
+  const uint64_t nv = n / 16u;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    const u32x4 x = *reinterpret_cast<const u32x4a*>(a + 16u * i);
+    const u32x4 y = *reinterpret_cast<const u32x4a*>(b + 16u * i);
+    *reinterpret_cast<u32x4a*>(out + 16u * i) = x ^ y;
+  }
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n - 16u * nv) out[16u * nv + t] = a[16u * nv + t] ^ b[16u * nv + t];
+}
+
+}  // namespace dev
+}  // namespace cmpi

@@ -1,0 +1,195 @@
+// ring_host.hpp — include/cmpi_ring.h: the CTR mask ring of send.c:1162-1465 with the ring in
+// HBM.  Included at the end of cmpi_aead.hip (one translation unit; uses ctr_launch).
+// The bookkeeping below follows the reference statement by statement (oracle/ctr_ring_ref.c
+// is the CPU restatement the tests compare against); every byte moved is moved by a kernel.
+#pragma once
+#include "../../include/cmpi_ring.h"
+
+struct cmpi_ctr_ring {
+  const cmpi_ctx* ctx = nullptr;
+  uint8_t iv[16];
+  uint8_t* dring = nullptr;  // device ring
+  int max = 0, start = 0, end = 0, compute_size = 0;
+  unsigned long counter = 0, counter_needto_send = 0;
+  std::mutex mu;
+};
+
+namespace {
+
+int xor_launch(uint8_t* out, const uint8_t* a, const uint8_t* b, size_t n, hipStream_t st) {
+  if (n == 0) return CMPI_OK;
+  const uint64_t nv = n / 16;
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((nv + 255) / 256, 4096));
+  hipLaunchKernelGGL(cmpi::dev::xor_bytes_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, out, a, b, (uint64_t)n);
+  HIP_TRY(hipGetLastError());
+  return CMPI_OK;
+}
+
+// keystream (in == nullptr) or in ^ keystream of the counters starting at IV_Count(iv, counter)
+int ring_ctr(const cmpi_ctr_ring* r, unsigned long counter, uint8_t* out, const uint8_t* in, size_t n, void* stream) {
+  uint8_t cb[16];
+  memcpy(cb, r->iv, 16);
+  cmpi_iv_count(cb, counter);
+  return ctr_launch(r->ctx, out, in, n, cb, stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+cmpi_ctr_ring* cmpi_ctr_ring_new(const cmpi_ctx* ctx, const uint8_t iv[16], size_t ring_bytes) {
+  if (!ctx || !iv) {
+    fail(CMPI_EINVAL, "null argument");
+    return nullptr;
+  }
+  if (ctx->dev_keys) {
+    fail(CMPI_EINVAL, "device-derived sub-key context supports GCM only");
+    return nullptr;
+  }
+  if (ring_bytes < 2048 || ring_bytes % 16 || ring_bytes > 0x40000000u) {
+    fail(CMPI_EINVAL, "ring_bytes must be a multiple of 16 in [2048, 1 GiB]");
+    return nullptr;
+  }
+  DeviceGuard dg(ctx->device);
+  auto* r = new cmpi_ctr_ring();
+  r->ctx = ctx;
+  memcpy(r->iv, iv, 16);
+  r->max = (int)ring_bytes;
+  if (hipMalloc(&r->dring, ring_bytes) != hipSuccess) {
+    fail(CMPI_ENOMEM, "hipMalloc ring failed");
+    delete r;
+    return nullptr;
+  }
+  return r;
+}
+
+void cmpi_ctr_ring_free(cmpi_ctr_ring* r) {
+  if (!r) return;
+  DeviceGuard dg(r->ctx->device);
+  if (r->dring) (void)hipFree(r->dring);
+  delete r;
+}
+
+int cmpi_ctr_ring_state(const cmpi_ctr_ring* r, uint64_t st[5]) {
+  if (!r || !st) return fail(CMPI_EINVAL, "null argument");
+  st[0] = (uint64_t)r->start;
+  st[1] = (uint64_t)r->end;
+  st[2] = (uint64_t)r->compute_size;
+  st[3] = r->counter;
+  st[4] = r->counter_needto_send;
+  return CMPI_OK;
+}
+
+// send.c:1162-1266
+int cmpi_ctr_ring_generate(cmpi_ctr_ring* r, size_t gen_bytes, void* stream) {
+  if (!r) return fail(CMPI_EINVAL, "null ring");
+  if (gen_bytes == 0 || gen_bytes > (size_t)r->max) return fail(CMPI_EINVAL, "gen_bytes out of range");
+  std::lock_guard<std::mutex> lk(r->mu);
+  DeviceGuard dg(r->ctx->device);
+  const int gen = (int)gen_bytes;
+  if (!(r->compute_size <= (r->max - gen - 1024))) return 0;
+  int blockamount = ((gen - 1) / 16) * 16 + 16;
+  int rc;
+  auto fill = [&](int amount) {
+    int e = ring_ctr(r, r->counter, r->dring + r->end, nullptr, (size_t)amount, stream);
+    r->compute_size += amount;
+    r->end += amount;
+    r->counter += (unsigned long)(amount / 16);
+    return e;
+  };
+  if (r->end > r->start && r->end + blockamount <= r->max) {
+    rc = fill(blockamount);
+  } else if ((r->end > r->start && r->end + blockamount > r->max) || (r->end == r->start && r->compute_size == 0)) {
+    const int tempamount = r->max - r->end;
+    if (blockamount > tempamount) {
+      if (tempamount && (rc = fill(tempamount))) return rc;
+      blockamount -= tempamount;
+      r->end = 0;
+    }
+    rc = fill(blockamount);
+  } else if (r->end < r->start && blockamount + r->end < r->start) {
+    rc = fill(blockamount);
+  } else {  // the reference prints ___ERROR___ in generation and exits (send.c:1253-1262)
+    return fail(CMPI_EINVAL, "mask ring state inconsistent (start %d end %d size %d)", r->start, r->end,
+                r->compute_size);
+  }
+  return rc ? rc : 1;
+}
+
+// send.c:1273-1465
+int cmpi_ctr_ring_encrypt(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_t n, void* stream) {
+  if (!r) return fail(CMPI_EINVAL, "null ring");
+  if (n == 0) return CMPI_OK;
+  if (!out || !in) return fail(CMPI_EINVAL, "null buffer");
+  if (n > 0x7FFFFFFFu) return fail(CMPI_EINVAL, "message larger than INT_MAX");
+  std::lock_guard<std::mutex> lk(r->mu);
+  DeviceGuard dg(r->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  const int enc_datasize = (int)n;
+  int how_much_generate, temporary_datasize, datasize;
+  if (enc_datasize > r->compute_size) {
+    how_much_generate = enc_datasize - r->compute_size;
+    datasize = temporary_datasize = r->compute_size;
+  } else {
+    how_much_generate = 0;
+    temporary_datasize = datasize = enc_datasize;
+  }
+  int rc;
+  if (r->compute_size > 0) {
+    if (r->end > r->start) {
+      const int tempamount = (r->start + datasize <= r->end) ? datasize : r->end - r->start;
+      if ((rc = xor_launch(out, r->dring + r->start, in, (size_t)tempamount, st))) return rc;
+      r->start += ((tempamount - 1) / 16) * 16 + 16;
+      if (r->start >= r->max) r->start = 0;
+      r->compute_size -= ((tempamount - 1) / 16) * 16 + 16;
+      r->counter_needto_send += (unsigned long)(((tempamount - 1) / 16) + 1);
+    } else if (r->end < r->start) {
+      const int tempamount = r->max - r->start;
+      int tempnext = 0;
+      if (datasize > tempamount) {
+        if (tempamount) {
+          if ((rc = xor_launch(out, r->dring + r->start, in, (size_t)tempamount, st))) return rc;
+          tempnext = tempamount;
+        }
+        r->start = 0;
+        datasize -= tempamount;
+      }
+      if ((rc = xor_launch(out + tempnext, r->dring + r->start, in + tempnext, (size_t)datasize, st))) return rc;
+      if (datasize > 0) r->start += ((datasize - 1) / 16) * 16 + 16;
+      if (r->start >= r->max) r->start = 0;
+      r->compute_size -= ((temporary_datasize - 1) / 16) * 16 + 16;
+      r->counter_needto_send += (unsigned long)(((temporary_datasize - 1) / 16) + 1);
+    }
+  }
+  if (how_much_generate) {
+    if ((rc = ring_ctr(r, r->counter, out + temporary_datasize, in + temporary_datasize, (size_t)how_much_generate,
+                       stream)))
+      return rc;
+    r->counter += (unsigned long)((how_much_generate - 1) / 16 + 1);
+    r->counter_needto_send += (unsigned long)(((how_much_generate - 1) / 16) + 1);
+  }
+  return CMPI_OK;
+}
+
+// recv.c:954-1023
+int cmpi_ctr_mask_decrypt(const cmpi_ctx* ctx, uint8_t* out, const uint8_t* in, size_t n, const uint8_t* mask,
+                          size_t mask_len, const uint8_t iv[16], uint64_t counter, void* stream) {
+  if (!ctx || !iv) return fail(CMPI_EINVAL, "null argument");
+  if (n == 0) return CMPI_OK;
+  if (!out || !in || (!mask && mask_len)) return fail(CMPI_EINVAL, "null buffer");
+  DeviceGuard dg(ctx->device);
+  const size_t len = std::min(n, mask_len);
+  int rc = xor_launch(out, mask, in, len, (hipStream_t)stream);
+  if (rc || n == len) return rc;
+  uint8_t cb[16];
+  memcpy(cb, iv, 16);
+  cmpi_iv_count(cb, (unsigned long)counter);
+  return ctr_launch(ctx, out + len, in + len, n - len, cb, stream);
+}
+
+int cmpi_xor_bytes(uint8_t* out, const uint8_t* a, const uint8_t* b, size_t n, void* stream) {
+  if (n && (!out || !a || !b)) return fail(CMPI_EINVAL, "null buffer");
+  return xor_launch(out, a, b, n, (hipStream_t)stream);
+}
+
+}  // extern "C"

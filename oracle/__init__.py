@@ -196,3 +196,41 @@ def seal602(key: bytes, small_key: bytes, pt: bytes, rand16: bytes, series_threa
     wire = (ctypes.c_uint8 * max(1, p.wire_bytes))(*([wire_fill] * max(1, p.wire_bytes)))
     lib().orc_602_seal(_buf(key), _buf(small_key), ctypes.byref(p), _buf(rand16), _buf(pt) if pt else None, hdr, wire)
     return bytes(hdr), bytes(wire)[: p.wire_bytes]
+
+
+# ---------------------------------------------------------------- CTR mask ring (send.c:1162-1465)
+class _Ring(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_uint8 * 16), ("iv", ctypes.c_uint8 * 16), ("buf", ctypes.c_void_p),
+                ("max", ctypes.c_int), ("start", ctypes.c_int), ("end", ctypes.c_int), ("compute_size", ctypes.c_int),
+                ("counter", ctypes.c_ulong), ("counter_needto_send", ctypes.c_ulong)]
+
+
+class Ring:
+    """The reference's enc_common_buffer state machine (generateCommonEncMask /
+    encryption_common_counter) over a ring of `max_bytes`."""
+
+    def __init__(self, key: bytes, iv: bytes, max_bytes: int = 8 << 20):
+        self._mem = (ctypes.c_uint8 * max_bytes)()
+        self._r = _Ring()
+        lib().orc_ring_init(ctypes.byref(self._r), _buf(key), _buf(iv), self._mem, max_bytes)
+
+    def generate(self, nbytes: int) -> int:
+        return lib().orc_ring_generate(ctypes.byref(self._r), nbytes)
+
+    def encrypt(self, data: bytes) -> bytes:
+        out = (ctypes.c_uint8 * max(1, len(data)))()
+        lib().orc_ring_encrypt(ctypes.byref(self._r), _buf(data) if data else None, len(data), out)
+        return bytes(out)[: len(data)]
+
+    def state(self) -> dict:
+        r = self._r
+        return {"start": r.start, "end": r.end, "compute_size": r.compute_size, "counter": r.counter,
+                "counter_needto_send": r.counter_needto_send}
+
+
+def mask_decrypt(key: bytes, iv: bytes, counter: int, mask: bytes, data: bytes) -> bytes:
+    """recv.c:954-1023 decryption_common_counter_ivflag."""
+    out = (ctypes.c_uint8 * max(1, len(data)))()
+    lib().orc_mask_decrypt(_buf(key), _buf(iv), ctypes.c_ulong(counter), _buf(mask) if mask else None, len(mask),
+                           _buf(data) if data else None, len(data), out)
+    return bytes(out)[: len(data)]
