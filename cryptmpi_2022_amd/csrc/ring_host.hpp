@@ -119,8 +119,9 @@ int cmpi_ctr_ring_generate(cmpi_ctr_ring* r, size_t gen_bytes, void* stream) {
 // send.c:1273-1465
 int cmpi_ctr_ring_encrypt(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_t n, void* stream) {
   if (!r) return fail(CMPI_EINVAL, "null ring");
-  if (n == 0) return CMPI_OK;
-  if (!out || !in) return fail(CMPI_EINVAL, "null buffer");
+  // n == 0 is not a no-op: like the reference, it retires one 16-byte ring block
+  // (((0 - 1) / 16) * 16 + 16 == 16, send.c:1331-1335).
+  if (n && (!out || !in)) return fail(CMPI_EINVAL, "null buffer");
   if (n > 0x7FFFFFFFu) return fail(CMPI_EINVAL, "message larger than INT_MAX");
   std::lock_guard<std::mutex> lk(r->mu);
   DeviceGuard dg(r->ctx->device);
