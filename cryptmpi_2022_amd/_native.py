@@ -51,6 +51,8 @@ _SIGS = {
     "cmpi_ctx_rekey_subkey": ([_P, _P, _P, _P], _I),
     "cmpi_ctx_free": ([_P], None),
     "cmpi_ctx_device": ([_P], _I),
+    "cmpi_host_register": ([_P, _S], _I),
+    "cmpi_host_unregister": ([_P], _I),
     "cmpi_gcm_workspace_size": ([_P, _S, _S], _S),
     "cmpi_gcm_seal_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
     "cmpi_gcm_open_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P, _P], _I),
@@ -92,6 +94,7 @@ _SIGS = {
     "cmpi_debug_set_ctr_lds": ([_I], None),
     "cmpi_debug_set_gcm_ablation": ([_I], None),
     "cmpi_debug_set_sched": ([_I], None),
+    "cmpi_debug_set_host_chunk": ([_S], None),
     "cmpi_debug_gcm_plan": ([_P, _S, _S, _P], _I),
 }
 

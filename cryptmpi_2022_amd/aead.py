@@ -127,28 +127,28 @@ class AeadCtx(_Ctx):
 
     # ------------------------------------------------------------ host (EVP_AEAD_CTX_seal/open)
     def seal_host_batch(self, nonces: np.ndarray, pt: np.ndarray) -> np.ndarray:
-        """(N,12) nonces, (N,n) plaintexts (host) -> (N, n+16) ct||tag, via pinned-free staging."""
-        if not self._gcm:
-            raise NotImplementedError("host staging path is GCM-only")
+        """(N,12) nonces, (N,n) plaintexts (host) -> (N, n+16) ct||tag through the pipelined host
+        path (chunked H2D / kernel / D2H on three streams)."""
         nrec, n = pt.shape
         out = np.empty((nrec, n + TAG_LEN), np.uint8)
         pt = np.ascontiguousarray(pt)
         nonces = np.ascontiguousarray(nonces)
-        N.check(N.lib().cmpi_gcm_seal_host(self._h, out.ctypes.data, out.strides[0], pt.ctypes.data,
-                                           max(pt.strides[0], 1), nonces.ctypes.data, 12, n, nrec))
+        fn = N.lib().cmpi_gcm_seal_host if self._gcm else N.lib().cmpi_ocb_seal_host
+        N.check(fn(self._h, out.ctypes.data, out.strides[0], pt.ctypes.data, max(pt.strides[0], 1),
+                   nonces.ctypes.data, 12, n, nrec))
         return out
 
     def open_host_batch(self, nonces: np.ndarray, ct_tag: np.ndarray):
-        if not self._gcm:
-            raise NotImplementedError("host staging path is GCM-only")
+        """-> (plaintexts, status): status[i] 1 ok / 0 forged (that record zero-filled)."""
         nrec, m = ct_tag.shape
         n = m - TAG_LEN
         out = np.empty((nrec, n), np.uint8)
         status = np.zeros(nrec, np.int32)
         ct_tag = np.ascontiguousarray(ct_tag)
         nonces = np.ascontiguousarray(nonces)
-        rc = N.lib().cmpi_gcm_open_host(self._h, out.ctypes.data, max(out.strides[0], 1), ct_tag.ctypes.data,
-                                        ct_tag.strides[0], nonces.ctypes.data, 12, n, nrec, status.ctypes.data)
+        fn = N.lib().cmpi_gcm_open_host if self._gcm else N.lib().cmpi_ocb_open_host
+        rc = fn(self._h, out.ctypes.data, max(out.strides[0], 1), ct_tag.ctypes.data, ct_tag.strides[0],
+                nonces.ctypes.data, 12, n, nrec, status.ctypes.data)
         if rc not in (N.CMPI_OK, N.CMPI_EAUTH):
             N.check(rc)
         return out, status

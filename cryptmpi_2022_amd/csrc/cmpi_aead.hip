@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -83,6 +84,15 @@ struct DevTables {
 
 }  // namespace
 
+// Host-path pipeline state of a context (aead_host): three streams, two staging slots.
+struct HostPipe {
+  hipStream_t s[3] = {nullptr, nullptr, nullptr};  // H2D, kernel, D2H
+  hipEvent_t in_ready[2], k_done[2], slot_free[2];
+  uint8_t* buf = nullptr;
+  size_t cap = 0;
+  bool init = false;
+};
+
 struct cmpi_ctx {
   int alg = 0;
   int device = 0;
@@ -104,6 +114,8 @@ struct cmpi_ctx {
   mutable uint8_t* stage = nullptr;
   mutable size_t stage_cap = 0;
   mutable hipStream_t hstream = nullptr;
+  mutable std::mutex hmu;                 // host-path pipeline (aead_host)
+  std::unique_ptr<HostPipe> pipe{new HostPipe()};
 };
 
 namespace {
@@ -450,6 +462,13 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
 }
 
 // ---------------------------------------------------------------- host staging
+// Host-memory batches (the *_host entry points: CryptMPI's buffers are host memory bound for a
+// NIC).  The batch is cut into chunks of ~g_host_chunk bytes pipelined over
+// three streams with two staging slots:  H2D(i+1) | kernel(i) | D2H(i-1)  overlap, the slot of
+// chunk i is reused by chunk i+2 once D2H(i) completed.  Pinned host buffers (hipHostMalloc /
+// cmpi_host_register) move by DMA at PCIe rate; pageable ones are staged by the HIP runtime.
+std::atomic<size_t> g_host_chunk{(size_t)8 << 20};
+
 template <bool DEC, bool OCB>
 int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
               const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status) {
@@ -459,35 +478,63 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
   if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
     return fail(CMPI_EINVAL, "stride smaller than record");
+  if (nrec == 1) in_stride = in_rec, out_stride = out_rec, nonce_stride = 12;
   DeviceGuard dg(c->device);
-  std::unique_lock<std::mutex> lk(c->mu);  // staging buffers are per ctx
-  if (!c->hstream) HIP_TRY(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
+  std::unique_lock<std::mutex> lk(c->hmu);  // the pipeline and its staging are per ctx
+  HostPipe& P = *c->pipe;
+  if (!P.init) {
+    for (auto& st : P.s) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+      HIP_TRY(hipEventCreateWithFlags(&P.in_ready[i], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&P.k_done[i], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&P.slot_free[i], hipEventDisableTiming));
+    }
+    P.init = true;
+  }
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t ip = up16(in_rec), op = up16(out_rec);
-  const size_t in_b = ip * nrec, out_b = op * nrec, n_b = 16 * nrec, st_b = up16(4 * nrec);
-  int rc = ensure_buf((void**)&c->stage, &c->stage_cap, in_b + out_b + n_b + st_b);
-  if (rc) return rc;
-  uint8_t* d_in = c->stage;
-  uint8_t* d_out = d_in + in_b;
-  uint8_t* d_n = d_out + out_b;
-  int32_t* d_st = reinterpret_cast<int32_t*>(d_n + n_b);
-  hipStream_t s = c->hstream;
-  if (in_rec) HIP_TRY(hipMemcpy2DAsync(d_in, ip, in, nrec > 1 ? in_stride : in_rec, in_rec, nrec, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpy2DAsync(d_n, 16, nonces, nrec > 1 ? nonce_stride : 12, 12, nrec, hipMemcpyHostToDevice, s));
-  lk.unlock();  // the batch call takes the lock itself for its scratch
-  if (OCB)
-    rc = ocb_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nrec, DEC ? d_st : nullptr, nullptr, s);
-  else
-    rc = gcm_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nrec, DEC ? d_st : nullptr, nullptr, s);
-  lk.lock();
-  if (rc) return rc;
-  if (out_rec) HIP_TRY(hipMemcpy2DAsync(out, nrec > 1 ? out_stride : out_rec, d_out, op, out_rec, nrec, hipMemcpyDeviceToHost, s));
-  std::vector<int32_t> hst;
-  if (DEC) {
-    hst.resize(nrec);
-    HIP_TRY(hipMemcpyAsync(hst.data(), d_st, 4 * nrec, hipMemcpyDeviceToHost, s));
+  const size_t per = std::max<size_t>(1, g_host_chunk.load() / std::max<size_t>(std::max(ip, op), 16));
+  const size_t K = std::min(per, nrec);  // records per chunk
+  const size_t in_b = ip * K, out_b = op * K, n_b = 16 * K, st_b = up16(4 * K);
+  const size_t slot_b = in_b + out_b + n_b + st_b;
+  if (P.cap < 2 * slot_b) {
+    HIP_TRY(hipStreamSynchronize(P.s[2]));
+    if (P.buf) (void)hipFree(P.buf);
+    P.buf = nullptr;
+    P.cap = 0;
+    if (hipMalloc(&P.buf, 2 * slot_b) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc staging failed");
+    P.cap = 2 * slot_b;
   }
-  HIP_TRY(hipStreamSynchronize(s));
+  std::vector<int32_t> hst(DEC ? nrec : 0);
+  const size_t nchunks = (nrec + K - 1) / K;
+  int rc = CMPI_OK;
+  for (size_t ci = 0; ci < nchunks && !rc; ++ci) {
+    const int sl = (int)(ci & 1);
+    const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
+    uint8_t* d_in = P.buf + sl * slot_b;
+    uint8_t* d_out = d_in + in_b;
+    uint8_t* d_n = d_out + out_b;
+    int32_t* d_st = reinterpret_cast<int32_t*>(d_n + n_b);
+    if (ci >= 2) HIP_TRY(hipStreamWaitEvent(P.s[0], P.slot_free[sl], 0));
+    if (in_rec)
+      HIP_TRY(hipMemcpy2DAsync(d_in, ip, in + r0 * in_stride, in_stride, in_rec, nr, hipMemcpyHostToDevice, P.s[0]));
+    HIP_TRY(hipMemcpy2DAsync(d_n, 16, nonces + r0 * nonce_stride, nonce_stride, 12, nr, hipMemcpyHostToDevice, P.s[0]));
+    HIP_TRY(hipEventRecord(P.in_ready[sl], P.s[0]));
+    HIP_TRY(hipStreamWaitEvent(P.s[1], P.in_ready[sl], 0));
+    if (OCB)
+      rc = ocb_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nr, DEC ? d_st : nullptr, nullptr, P.s[1]);
+    else
+      rc = gcm_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nr, DEC ? d_st : nullptr, nullptr, P.s[1]);
+    if (rc) break;
+    HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
+    HIP_TRY(hipStreamWaitEvent(P.s[2], P.k_done[sl], 0));
+    if (out_rec)
+      HIP_TRY(hipMemcpy2DAsync(out + r0 * out_stride, out_stride, d_out, op, out_rec, nr, hipMemcpyDeviceToHost, P.s[2]));
+    if (DEC) HIP_TRY(hipMemcpyAsync(hst.data() + r0, d_st, 4 * nr, hipMemcpyDeviceToHost, P.s[2]));
+    HIP_TRY(hipEventRecord(P.slot_free[sl], P.s[2]));
+  }
+  for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
+  if (rc) return rc;
   if (DEC) {
     size_t bad = 0;
     for (size_t i = 0; i < nrec; ++i) bad += hst[i] == 0;
@@ -656,6 +703,18 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
+  if (c->pipe) {
+    HostPipe& P = *c->pipe;
+    if (P.init) {
+      for (auto& st : P.s) (void)hipStreamDestroy(st);
+      for (int i = 0; i < 2; ++i) {
+        (void)hipEventDestroy(P.in_ready[i]);
+        (void)hipEventDestroy(P.k_done[i]);
+        (void)hipEventDestroy(P.slot_free[i]);
+      }
+    }
+    if (P.buf) (void)hipFree(P.buf);
+  }
   if (c->dt) (void)hipFree(c->dt);
   memset(c->key, 0, 16);
   delete c;
@@ -663,7 +722,20 @@ void cmpi_ctx_free(cmpi_ctx* c) {
 
 int cmpi_ctx_device(const cmpi_ctx* c) { return c ? c->device : -1; }
 
+int cmpi_host_register(void* ptr, size_t bytes) {
+  if (!ptr || !bytes) return fail(CMPI_EINVAL, "null/empty buffer");
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  return CMPI_OK;
+}
+
+int cmpi_host_unregister(void* ptr) {
+  if (!ptr) return fail(CMPI_EINVAL, "null buffer");
+  HIP_TRY(hipHostUnregister(ptr));
+  return CMPI_OK;
+}
+
 void cmpi_debug_set_sched(int mode) { g_sched.store(mode & 7); }
+void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)8 << 20)); }
 void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 7); }
 
 void cmpi_debug_set_ctr_lds(int lds_bytes) {

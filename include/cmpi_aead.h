@@ -86,6 +86,10 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx *dst, const cmpi_ctx *base, const uint8_t v[1
 cmpi_ctx *cmpi_ctx_new_subkey(const cmpi_ctx *base, const uint8_t v[16]);
 void cmpi_ctx_free(cmpi_ctx *ctx);
 int cmpi_ctx_device(const cmpi_ctx *ctx);
+/* Pin (page-lock) a host buffer for DMA, e.g. MPI send/receive buffers reused across calls, so
+ * the *_host calls move it at PCIe rate; unregister before freeing it. */
+int cmpi_host_register(void *ptr, size_t bytes);
+int cmpi_host_unregister(void *ptr);
 
 /* ---------------- AES-128-GCM, uniform batches (device pointers) ----------------
  * Record i (0 <= i < nrec):

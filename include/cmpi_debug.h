@@ -25,6 +25,8 @@ void cmpi_debug_set_gcm_ablation(int mode);
 void cmpi_debug_set_ctr_lds(int lds_bytes);
 /* Wave-priority rotation in the main loops (default 7): bit 0 GCM, bit 1 CTR, bit 2 OCB. */
 void cmpi_debug_set_sched(int mode);
+/* Chunk bytes of the pipelined host path (*_host calls; 0 = default 8 MiB). */
+void cmpi_debug_set_host_chunk(size_t bytes);
 /* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}. */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);
 

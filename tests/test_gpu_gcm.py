@@ -299,3 +299,35 @@ def test_device_keyed_ctx_rejects_ctr():
     sub = aead.AeadCtx.derive_subkey(base, bytes(range(16)))
     rc = aead.N.lib().cmpi_ctr_keystream(sub.handle, None, 1, (aead.ctypes.c_uint8 * 16)(), None)
     assert rc == aead.N.CMPI_EINVAL
+
+
+@pytest.mark.parametrize("alg", ["aes-128-gcm", "aes-128-ocb"])
+@pytest.mark.parametrize("chunk", [4096, 65536, 0])
+def test_host_pipeline_chunks(alg, chunk):
+    """The pipelined host path (3 streams, 2 staging slots) across many chunks, ragged last chunk,
+    forged records reported per record and zero-filled, for pinned (registered) and pageable."""
+    n, nrec = 1000, 301
+    pt = records(0x5151 + chunk, nrec, n)
+    nonces = random_nonces(0x5152, nrec)
+    ctx = aead.AeadCtx(KEY, alg)
+    want = (oracle.gcm_seal_batch if alg == "aes-128-gcm" else oracle.ocb_seal_batch)(KEY, nonces, pt)
+    try:
+        aead.N.lib().cmpi_debug_set_host_chunk(chunk)
+        got = ctx.seal_host_batch(nonces, pt)
+        assert np.array_equal(got, want)
+        forged = got.copy()
+        forged[[0, 150, 300], -1] ^= 1
+        back, st = ctx.open_host_batch(nonces, forged)
+        assert list(np.nonzero(st == 0)[0]) == [0, 150, 300]
+        assert (back[[0, 150, 300]] == 0).all() and np.array_equal(back[1:150], pt[1:150])
+        back, st = ctx.open_host_batch(nonces, got)
+        assert (st == 1).all() and np.array_equal(back, pt)
+        # registered (pinned) host buffers
+        buf = np.ascontiguousarray(pt)
+        assert aead.N.lib().cmpi_host_register(buf.ctypes.data, buf.nbytes) == 0
+        try:
+            assert np.array_equal(ctx.seal_host_batch(nonces, buf), want)
+        finally:
+            aead.N.lib().cmpi_host_unregister(buf.ctypes.data)
+    finally:
+        aead.N.lib().cmpi_debug_set_host_chunk(0)
