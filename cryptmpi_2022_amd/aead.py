@@ -58,9 +58,9 @@ class _Ctx:
         self.device = N.lib().cmpi_ctx_device(self._h)
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and N is not None and N.lib is not None:  # N is None at interpreter exit
             N.lib().cmpi_ctx_free(self._h)
-            self._h = None
+        self._h = None
 
     __del__ = close
 

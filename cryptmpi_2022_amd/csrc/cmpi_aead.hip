@@ -20,6 +20,7 @@
 #include <vector>
 
 #include <sys/random.h>
+#include <cstdlib>
 
 #include "../../include/cmpi_aead.h"
 #include "../../include/cmpi_coll.h"
@@ -88,7 +89,8 @@ struct DevTables {
 struct HostPipe {
   hipStream_t s[3] = {nullptr, nullptr, nullptr};  // H2D, kernel, D2H
   hipEvent_t in_ready[2], k_done[2], slot_free[2];
-  uint8_t* buf = nullptr;
+  uint8_t* buf = nullptr;   // device staging, 2 slots
+  uint8_t* hbuf = nullptr;  // pinned host staging, 2 slots (pageable user buffers)
   size_t cap = 0;
   bool init = false;
 };
@@ -469,6 +471,19 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
 // cmpi_host_register) move by DMA at PCIe rate; pageable ones are staged by the HIP runtime.
 std::atomic<size_t> g_host_chunk{(size_t)8 << 20};
 
+// true when p lies in page-locked host memory (hipHostMalloc / hipHostRegister): it can be the
+// direct source/target of an asynchronous DMA.  Pageable memory is never handed to async copies
+// (the runtime's pageable path under concurrent streams faulted in testing, round 1): it goes
+// through our pinned staging slots with a CPU pack/unpack overlapped with the other chunks.
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
 template <bool DEC, bool OCB>
 int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
               const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status) {
@@ -497,42 +512,97 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const size_t K = std::min(per, nrec);  // records per chunk
   const size_t in_b = ip * K, out_b = op * K, n_b = 16 * K, st_b = up16(4 * K);
   const size_t slot_b = in_b + out_b + n_b + st_b;
-  if (P.cap < 2 * slot_b) {
-    HIP_TRY(hipStreamSynchronize(P.s[2]));
+  if (P.cap < slot_b) {
+    for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
     if (P.buf) (void)hipFree(P.buf);
-    P.buf = nullptr;
+    if (P.hbuf) (void)hipHostFree(P.hbuf);
+    P.buf = P.hbuf = nullptr;
     P.cap = 0;
     if (hipMalloc(&P.buf, 2 * slot_b) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc staging failed");
-    P.cap = 2 * slot_b;
+    if (hipHostMalloc(&P.hbuf, 2 * slot_b, hipHostMallocDefault) != hipSuccess) {
+      (void)hipFree(P.buf);
+      P.buf = nullptr;
+      return fail(CMPI_ENOMEM, "hipHostMalloc staging failed");
+    }
+    P.cap = slot_b;
   }
+  const bool in_pinned = in_rec && is_pinned(in), out_pinned = out_rec && is_pinned(out);
   std::vector<int32_t> hst(DEC ? nrec : 0);
   const size_t nchunks = (nrec + K - 1) / K;
+  static const bool dbg_sync = getenv("CMPI_DEBUG_SYNC") != nullptr;  // diagnose: sync + check each step
+  auto step = [&](const char* what, size_t ci) -> int {
+    if (!dbg_sync) return CMPI_OK;
+    for (auto& st : P.s) {
+      const hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return fail(CMPI_EHIP, "%s (chunk %zu): %s", what, ci, hipGetErrorString(e));
+    }
+    return CMPI_OK;
+  };
+  auto layout = [&](int sl, uint8_t* base) {
+    struct L {
+      uint8_t *in, *out, *n;
+      int32_t* st;
+    } l;
+    l.in = base + sl * slot_b;
+    l.out = l.in + in_b;
+    l.n = l.out + out_b;
+    l.st = reinterpret_cast<int32_t*>(l.n + n_b);
+    return l;
+  };
+  // copy chunk ci's outputs from the pinned slot to the user's buffers (after its D2H)
+  auto unpack = [&](size_t ci) -> int {
+    const int sl = (int)(ci & 1);
+    const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
+    HIP_TRY(hipEventSynchronize(P.slot_free[sl]));
+    const auto h = layout(sl, P.hbuf);
+    if (out_rec && !out_pinned)
+      for (size_t i = 0; i < nr; ++i) memcpy(out + (r0 + i) * out_stride, h.out + i * op, out_rec);
+    if (DEC) memcpy(hst.data() + r0, h.st, 4 * nr);
+    return CMPI_OK;
+  };
   int rc = CMPI_OK;
   for (size_t ci = 0; ci < nchunks && !rc; ++ci) {
     const int sl = (int)(ci & 1);
     const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
-    uint8_t* d_in = P.buf + sl * slot_b;
-    uint8_t* d_out = d_in + in_b;
-    uint8_t* d_n = d_out + out_b;
-    int32_t* d_st = reinterpret_cast<int32_t*>(d_n + n_b);
+    const auto d = layout(sl, P.buf);
+    const auto h = layout(sl, P.hbuf);
+    // slot sl was last used by chunk ci-2: its H2D must have read the pinned inputs and its
+    // outputs must have been unpacked (done at iteration ci-1) before we overwrite them
+    if (ci >= 2) HIP_TRY(hipEventSynchronize(P.in_ready[sl]));
+    if (in_rec && !in_pinned)
+      for (size_t i = 0; i < nr; ++i) memcpy(h.in + i * ip, in + (r0 + i) * in_stride, in_rec);
+    for (size_t i = 0; i < nr; ++i) memcpy(h.n + 16 * i, nonces + (r0 + i) * nonce_stride, 12);
     if (ci >= 2) HIP_TRY(hipStreamWaitEvent(P.s[0], P.slot_free[sl], 0));
-    if (in_rec)
-      HIP_TRY(hipMemcpy2DAsync(d_in, ip, in + r0 * in_stride, in_stride, in_rec, nr, hipMemcpyHostToDevice, P.s[0]));
-    HIP_TRY(hipMemcpy2DAsync(d_n, 16, nonces + r0 * nonce_stride, nonce_stride, 12, nr, hipMemcpyHostToDevice, P.s[0]));
+    if (in_rec) {
+      if (in_pinned)
+        HIP_TRY(hipMemcpy2DAsync(d.in, ip, in + r0 * in_stride, in_stride, in_rec, nr, hipMemcpyHostToDevice, P.s[0]));
+      else
+        HIP_TRY(hipMemcpyAsync(d.in, h.in, ip * nr, hipMemcpyHostToDevice, P.s[0]));
+    }
+    HIP_TRY(hipMemcpyAsync(d.n, h.n, 16 * nr, hipMemcpyHostToDevice, P.s[0]));
+    if ((rc = step("H2D", ci))) break;
     HIP_TRY(hipEventRecord(P.in_ready[sl], P.s[0]));
     HIP_TRY(hipStreamWaitEvent(P.s[1], P.in_ready[sl], 0));
     if (OCB)
-      rc = ocb_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nr, DEC ? d_st : nullptr, nullptr, P.s[1]);
+      rc = ocb_batch<DEC>(c, d.out, op, d.in, ip, d.n, 16, len, nr, DEC ? d.st : nullptr, nullptr, P.s[1]);
     else
-      rc = gcm_batch<DEC>(c, d_out, op, d_in, ip, d_n, 16, len, nr, DEC ? d_st : nullptr, nullptr, P.s[1]);
+      rc = gcm_batch<DEC>(c, d.out, op, d.in, ip, d.n, 16, len, nr, DEC ? d.st : nullptr, nullptr, P.s[1]);
     if (rc) break;
+    if ((rc = step("kernel", ci))) break;
     HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
     HIP_TRY(hipStreamWaitEvent(P.s[2], P.k_done[sl], 0));
-    if (out_rec)
-      HIP_TRY(hipMemcpy2DAsync(out + r0 * out_stride, out_stride, d_out, op, out_rec, nr, hipMemcpyDeviceToHost, P.s[2]));
-    if (DEC) HIP_TRY(hipMemcpyAsync(hst.data() + r0, d_st, 4 * nr, hipMemcpyDeviceToHost, P.s[2]));
+    if (out_rec) {
+      if (out_pinned)
+        HIP_TRY(hipMemcpy2DAsync(out + r0 * out_stride, out_stride, d.out, op, out_rec, nr, hipMemcpyDeviceToHost, P.s[2]));
+      else
+        HIP_TRY(hipMemcpyAsync(h.out, d.out, op * nr, hipMemcpyDeviceToHost, P.s[2]));
+    }
+    if (DEC) HIP_TRY(hipMemcpyAsync(h.st, d.st, 4 * nr, hipMemcpyDeviceToHost, P.s[2]));
+    if ((rc = step("D2H", ci))) break;
     HIP_TRY(hipEventRecord(P.slot_free[sl], P.s[2]));
+    if (ci >= 1 && (rc = unpack(ci - 1))) break;  // overlaps the GPU work of chunk ci
   }
+  if (!rc) rc = unpack(nchunks - 1);
   for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
   if (rc) return rc;
   if (DEC) {
@@ -699,6 +769,10 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
 void cmpi_ctx_free(cmpi_ctx* c) {
   if (!c) return;
   DeviceGuard dg(c->device);
+  // Work of this context may still be in flight on any caller stream (stream-ordered batch
+  // calls, the key-setup kernel of a derived sub-key): drain the device before its tables,
+  // scratch and staging go back to the allocator.
+  (void)hipDeviceSynchronize();
   for (auto& kv : c->pw) (void)hipFree(kv.second.first);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->stage) (void)hipFree(c->stage);
@@ -714,6 +788,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
       }
     }
     if (P.buf) (void)hipFree(P.buf);
+    if (P.hbuf) (void)hipHostFree(P.hbuf);
   }
   if (c->dt) (void)hipFree(c->dt);
   memset(c->key, 0, 16);

@@ -66,6 +66,7 @@ cmpi_ctr_ring* cmpi_ctr_ring_new(const cmpi_ctx* ctx, const uint8_t iv[16], size
 void cmpi_ctr_ring_free(cmpi_ctr_ring* r) {
   if (!r) return;
   DeviceGuard dg(r->ctx->device);
+  (void)hipDeviceSynchronize();  // ring fills / consumptions may still be in flight
   if (r->dring) (void)hipFree(r->dring);
   delete r;
 }

@@ -17,9 +17,9 @@ class CtrRing:
         self._h = h
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and N is not None and N.lib is not None:
             N.lib().cmpi_ctr_ring_free(self._h)
-            self._h = None
+        self._h = None
 
     __del__ = close
 

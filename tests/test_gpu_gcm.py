@@ -299,6 +299,9 @@ def test_device_keyed_ctx_rejects_ctr():
     sub = aead.AeadCtx.derive_subkey(base, bytes(range(16)))
     rc = aead.N.lib().cmpi_ctr_keystream(sub.handle, None, 1, (aead.ctypes.c_uint8 * 16)(), None)
     assert rc == aead.N.CMPI_EINVAL
+    import torch
+
+    torch.cuda.synchronize()  # the key-setup kernel is asynchronous
 
 
 @pytest.mark.parametrize("alg", ["aes-128-gcm", "aes-128-ocb"])
