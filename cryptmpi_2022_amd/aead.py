@@ -200,6 +200,12 @@ def force_plan(lanes_per_record: int = 0, segments: int = 0) -> None:
     N.lib().cmpi_debug_force_plan(lanes_per_record, segments)
 
 
+def force_wide(mode: int = 0, steps: int = 0) -> None:
+    """Test hook: wide GCM decomposition 0 automatic / 1 always (when legal) / -1 never;
+    steps per chunk (0 = automatic)."""
+    N.lib().cmpi_debug_force_wide(mode, steps)
+
+
 def gcm_plan(ctx: AeadCtx, length: int, nrec: int):
     out = (ctypes.c_uint32 * 4)()
     N.check(N.lib().cmpi_debug_gcm_plan(ctx.handle, length, nrec, out))

@@ -110,6 +110,9 @@ struct cmpi_ctx {
   // per-G segment power tables, H^{kG}
   mutable std::mutex mu;
   mutable std::map<uint32_t, std::pair<u32x4*, uint32_t>> pw;
+  // wide decomposition: byte table of H^64 and per-(S, nch) lane/chunk weights (lazy)
+  mutable u32x4* h64tab = nullptr;
+  mutable std::map<std::pair<uint32_t, uint32_t>, u32x4*> wtab;
   // internal scratch (partials, status) and staging for *_host
   mutable void* scratch = nullptr;
   mutable size_t scratch_cap = 0;
@@ -150,11 +153,15 @@ int set_lds_attr(const void* fn, int device, size_t lds) {
 struct GcmPlan {
   int L;
   uint32_t nb, nseg, G, r0;
+  bool wide = false;  // gcm_wide_kernel: nseg = chunks per record, G = 64*S X-blocks per chunk
+  uint32_t S = 0;
 };
 
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
+std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
+std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
 std::atomic<int> g_sched{7};         // wave-priority rotation: bit 0 GCM, bit 1 CTR, bit 2 OCB
 std::atomic<int> g_gcm_ablation{0};  // timing ablation of the L=4 seal kernel (tools/ablate.py)  // LDS requested by the CTR kernel (occupancy experiments)
@@ -177,6 +184,23 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   }
   if (g_force_L.load()) p.L = g_force_L.load();
   if (g_force_nseg.load()) nseg = std::min<uint64_t>(g_force_nseg.load(), nx);
+  // Wide decomposition when the lane-group plan leaves most of the chip idle (few long
+  // records: the naive collectives' p peer blocks).  Host-keyed contexts only (the chunk
+  // weights are built from H on the host); records need >= 64 data blocks.
+  const int fw = g_force_wide.load();
+  const bool wide_ok = !c->dev_keys && p.nb >= 64;
+  if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target && nx >= 1024))) {
+    uint64_t S = g_force_S.load();
+    if (!S) S = std::max<uint64_t>(4, (uint64_t)nrec * nx / (64ull * c->ncu * (kGcmThreads / 64)));
+    S = std::min<uint64_t>(S, (nx + 63) / 64);
+    p.wide = true;
+    p.S = (uint32_t)S;
+    p.L = 64;
+    p.G = (uint32_t)(64 * S);
+    p.nseg = (uint32_t)((nx + p.G - 1) / p.G);
+    p.r0 = (uint32_t)(nx - (uint64_t)(p.nseg - 1) * p.G);
+    return p;
+  }
   uint64_t G = (nx + nseg - 1) / nseg;
   nseg = (nx + G - 1) / G;
   p.G = (uint32_t)G;
@@ -187,8 +211,59 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
 
 // workspace: partials [nrec][nseg], E_K(J0) [nrec], and for device-keyed contexts H^{kG} [nseg]
 size_t gcm_ws_bytes(const cmpi_ctx* c, const GcmPlan& p, size_t nrec) {
+  if (p.wide) return (size_t)nrec * p.nseg * 16;
   if (p.nseg <= 1) return 0;
   return (size_t)nrec * p.nseg * 16 + nrec * 16 + (c->dev_keys ? (size_t)p.nseg * 16 : 0);
+}
+
+// Byte table of H^64 (the wide kernel's Horner multiplier), built once per context.
+int get_h64tab(const cmpi_ctx* c, const u32x4** out) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->h64tab) {
+    std::vector<Blk> tab(4096);
+    cmpi::build_byte_table(cmpi::gf_pow(c->H, 64), tab.data());
+    u32x4* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 4096 * 16));
+    HIP_TRY(hipMemcpy(d, tab.data(), 4096 * 16, hipMemcpyHostToDevice));
+    c->h64tab = d;
+  }
+  *out = c->h64tab;
+  return CMPI_OK;
+}
+
+// Wide-chunk weights wtab[i*64 + q] = H^{(nch-1-i)*64S + 64 - q}, cached per (S, nch):
+// row nch-1 holds H^{64-q}; each earlier row is the next one times H^{64S} (byte-table multiply).
+int get_wtab(const cmpi_ctx* c, uint32_t S, uint32_t nch, const u32x4** out) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  auto key = std::make_pair(S, nch);
+  auto it = c->wtab.find(key);
+  if (it != c->wtab.end()) {
+    *out = it->second;
+    return CMPI_OK;
+  }
+  std::vector<Blk> mt(4096), w((size_t)nch * 64);
+  cmpi::build_byte_table(cmpi::gf_pow(c->H, 64ull * S), mt.data());
+  auto mul_t = [&](const Blk& x) {
+    Blk z{};
+    for (int p = 0; p < 16; ++p) {
+      const Blk& e = mt[(size_t)x.b[p] * 16 + p];
+      for (int b = 0; b < 16; ++b) z.b[b] ^= e.b[b];
+    }
+    return z;
+  };
+  Blk hq = cmpi::gf_one();  // H^{64-q} for q = 63 down to 0
+  for (int q = 63; q >= 0; --q) {
+    hq = cmpi::gf_mul(hq, c->H);
+    w[(size_t)(nch - 1) * 64 + q] = hq;
+  }
+  for (int64_t i = (int64_t)nch - 2; i >= 0; --i)
+    for (int q = 0; q < 64; ++q) w[(size_t)i * 64 + q] = mul_t(w[(size_t)(i + 1) * 64 + q]);
+  u32x4* d = nullptr;
+  HIP_TRY(hipMalloc(&d, w.size() * 16));
+  HIP_TRY(hipMemcpy(d, w.data(), w.size() * 16, hipMemcpyHostToDevice));
+  c->wtab[key] = d;
+  *out = d;
+  return CMPI_OK;
 }
 
 int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
@@ -287,6 +362,46 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   memcpy(a.nfix, ns.fix, sizeof a.nfix);
   a.sched = (uint32_t)g_sched.load();
   const u32x4* pw = nullptr;
+  if (p.wide) {
+    if ((uint64_t)nrec * p.nseg * 16 > 0xFFFFFFFFull) return fail(CMPI_EINVAL, "too many chunks");
+    uint8_t* ws = (uint8_t*)workspace;
+    if (!ws) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      int rc = ensure_buf(&c->scratch, &c->scratch_cap, gcm_ws_bytes(c, p, nrec));
+      if (rc) return rc;
+      ws = (uint8_t*)c->scratch;
+    }
+    a.partial = reinterpret_cast<u32x4*>(ws);
+    a.S = p.S;
+    a.nch = p.nseg;
+    int rc = get_h64tab(c, &a.htab);
+    if (!rc) rc = get_wtab(c, p.S, p.nseg, &a.wtab);
+    if (rc) return rc;
+    auto fn = cmpi::dev::gcm_wide_kernel<DEC>;
+    const size_t lds = 2 * 65536;
+    if ((rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds))) return rc;
+    const uint64_t waves = (uint64_t)nrec * p.nseg;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>((waves + kGcmThreads / 64 - 1) / (kGcmThreads / 64), (uint64_t)c->ncu));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
+    HIP_TRY(hipGetLastError());
+    cmpi::dev::GcmCombineArgs ca{};
+    ca.in = in;
+    ca.out = out;
+    ca.in_stride = in_stride;
+    ca.out_stride = out_stride;
+    ca.len = (uint32_t)len;
+    ca.nb = p.nb;
+    ca.nrec = (uint32_t)nrec;
+    ca.nseg = p.nseg;
+    ca.partial = a.partial;
+    ca.ekj0 = nullptr;  // inside chunk 0's partial
+    ca.pw = nullptr;    // partials are weighted in-kernel
+    ca.status = status;
+    hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(64), 0, st, ca);
+    HIP_TRY(hipGetLastError());
+    return CMPI_OK;
+  }
   if (p.nseg > 1) {
     uint8_t* ws = (uint8_t*)workspace;
     if (!ws) {
@@ -507,7 +622,14 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     P.init = true;
   }
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  const size_t ip = up16(in_rec), op = up16(out_rec);
+  const bool in_pinned = in_rec && is_pinned(in), out_pinned = out_rec && is_pinned(out);
+  // Device pitch = the user's stride when one flat DMA can move the chunk: inputs may carry
+  // small gaps (read and ignored), outputs only when they are dense (a flat D2H would overwrite
+  // the caller's bytes between records, e.g. the next record's nonce in the wire layout).
+  // hipMemcpy2DAsync on host memory runs far below the flat-copy PCIe rate (measured round 1).
+  const bool in_flat = in_pinned && (nrec == 1 || in_stride <= in_rec + 64);
+  const bool out_flat = out_pinned && (nrec == 1 || out_stride == out_rec);
+  const size_t ip = in_flat ? in_stride : up16(in_rec), op = out_flat ? out_stride : up16(out_rec);
   const size_t per = std::max<size_t>(1, g_host_chunk.load() / std::max<size_t>(std::max(ip, op), 16));
   const size_t K = std::min(per, nrec);  // records per chunk
   const size_t in_b = ip * K, out_b = op * K, n_b = 16 * K, st_b = up16(4 * K);
@@ -526,7 +648,6 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
     P.cap = slot_b;
   }
-  const bool in_pinned = in_rec && is_pinned(in), out_pinned = out_rec && is_pinned(out);
   std::vector<int32_t> hst(DEC ? nrec : 0);
   const size_t nchunks = (nrec + K - 1) / K;
   static const bool dbg_sync = getenv("CMPI_DEBUG_SYNC") != nullptr;  // diagnose: sync + check each step
@@ -574,7 +695,9 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     for (size_t i = 0; i < nr; ++i) memcpy(h.n + 16 * i, nonces + (r0 + i) * nonce_stride, 12);
     if (ci >= 2) HIP_TRY(hipStreamWaitEvent(P.s[0], P.slot_free[sl], 0));
     if (in_rec) {
-      if (in_pinned)
+      if (in_flat)
+        HIP_TRY(hipMemcpyAsync(d.in, in + r0 * in_stride, (nr - 1) * ip + in_rec, hipMemcpyHostToDevice, P.s[0]));
+      else if (in_pinned)
         HIP_TRY(hipMemcpy2DAsync(d.in, ip, in + r0 * in_stride, in_stride, in_rec, nr, hipMemcpyHostToDevice, P.s[0]));
       else
         HIP_TRY(hipMemcpyAsync(d.in, h.in, ip * nr, hipMemcpyHostToDevice, P.s[0]));
@@ -592,7 +715,9 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
     HIP_TRY(hipStreamWaitEvent(P.s[2], P.k_done[sl], 0));
     if (out_rec) {
-      if (out_pinned)
+      if (out_flat)
+        HIP_TRY(hipMemcpyAsync(out + r0 * out_stride, d.out, (nr - 1) * op + out_rec, hipMemcpyDeviceToHost, P.s[2]));
+      else if (out_pinned)
         HIP_TRY(hipMemcpy2DAsync(out + r0 * out_stride, out_stride, d.out, op, out_rec, nr, hipMemcpyDeviceToHost, P.s[2]));
       else
         HIP_TRY(hipMemcpyAsync(h.out, d.out, op * nr, hipMemcpyDeviceToHost, P.s[2]));
@@ -774,6 +899,8 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   // scratch and staging go back to the allocator.
   (void)hipDeviceSynchronize();
   for (auto& kv : c->pw) (void)hipFree(kv.second.first);
+  for (auto& kv : c->wtab) (void)hipFree(kv.second);
+  if (c->h64tab) (void)hipFree(c->h64tab);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
@@ -820,6 +947,11 @@ void cmpi_debug_set_ctr_lds(int lds_bytes) {
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
   g_force_L.store(lanes_per_record == 1 || lanes_per_record == 2 || lanes_per_record == 4 ? lanes_per_record : 0);
   g_force_nseg.store(segments);
+}
+
+void cmpi_debug_force_wide(int mode, uint32_t steps) {
+  g_force_wide.store(mode > 0 ? 1 : (mode < 0 ? -1 : 0));
+  g_force_S.store(steps);
 }
 
 int cmpi_debug_gcm_plan(const cmpi_ctx* c, size_t len, size_t nrec, uint32_t out[4]) {

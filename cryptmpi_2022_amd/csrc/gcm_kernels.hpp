@@ -52,6 +52,9 @@ struct GcmArgs {
   //     RAND_bytes nonce per message, send.c:294-311)
   uint32_t nmode, nctr0, nflag;
   uint32_t nfix[3];
+  // wide decomposition (gcm_wide_kernel): S steps per chunk, nch chunks per record, weights
+  const u32x4* wtab;
+  uint32_t S, nch;
   RoundKeys rk;
 };
 
@@ -67,6 +70,48 @@ __device__ __forceinline__ RoundKeys load_round_keys(const RoundKeys& arg, const
 
 __device__ __forceinline__ u32x4 ld_blk(const uint8_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
 __device__ __forceinline__ void st_blk(uint8_t* p, u32x4 v) { *reinterpret_cast<u32x4a*>(p) = v; }
+
+// Record r's 96-bit nonce as three LE words (see GcmArgs::nmode); `writer` (one lane of the
+// record, seal only) also writes the nonce / 5-byte prefix the framing puts on the wire.
+__device__ __forceinline__ void gcm_nonce(const GcmArgs& a, uint32_t r, bool writer, uint32_t& n0, uint32_t& n1,
+                                          uint32_t& n2) {
+  uint8_t* nb8 = const_cast<uint8_t*>(a.nonces) + (uint64_t)r * a.nonce_stride;
+  if (a.nmode == 0u) {
+    const u32a* np = reinterpret_cast<const u32a*>(nb8);
+    n0 = np[0];
+    n1 = np[1];
+    n2 = np[2];
+  } else if (a.nmode == 3u) {
+    n0 = a.nfix[0];
+    n1 = a.nfix[1];
+    n2 = a.nfix[2];
+    if (writer && nb8) {
+      u32a* np = reinterpret_cast<u32a*>(nb8);
+      np[0] = n0;
+      np[1] = n1;
+      np[2] = n2;
+    }
+  } else {
+    uint32_t f, c;
+    if (a.nmode == 1u) {
+      f = nb8[0];
+      c = ((uint32_t)nb8[1] << 24) | ((uint32_t)nb8[2] << 16) | ((uint32_t)nb8[3] << 8) | nb8[4];
+    } else {
+      f = a.nflag;
+      c = a.nctr0 + r;
+      if (writer) {
+        nb8[0] = (uint8_t)f;
+        nb8[1] = (uint8_t)(c >> 24);
+        nb8[2] = (uint8_t)(c >> 16);
+        nb8[3] = (uint8_t)(c >> 8);
+        nb8[4] = (uint8_t)c;
+      }
+    }
+    n0 = 0x30303030u;              // "0000"
+    n1 = 0x00303030u | (f << 24);  // "000" || flag
+    n2 = __builtin_bswap32(c);     // BE32 counter
+  }
+}
 
 // LDS: GHASH byte table [v][p] @0 (64 KiB), AES row image @64K (64 KiB), nibble tables of
 // H^1..H^L @128K (L x 8 KiB, L > 1).  L = 4 uses the whole 160 KiB of the CU.
@@ -106,44 +151,7 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
     const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
     uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
     uint32_t n0, n1, n2;
-    {
-      uint8_t* nb8 = const_cast<uint8_t*>(a.nonces) + (uint64_t)r * a.nonce_stride;
-      if (a.nmode == 0u) {
-        const u32a* np = reinterpret_cast<const u32a*>(nb8);
-        n0 = np[0];
-        n1 = np[1];
-        n2 = np[2];
-      } else if (a.nmode == 3u) {
-        n0 = a.nfix[0];
-        n1 = a.nfix[1];
-        n2 = a.nfix[2];
-        if (!DECRYPT && nb8 && s == 0u && q == 0u) {
-          u32a* np = reinterpret_cast<u32a*>(nb8);
-          np[0] = n0;
-          np[1] = n1;
-          np[2] = n2;
-        }
-      } else {
-        uint32_t f, c;
-        if (a.nmode == 1u) {
-          f = nb8[0];
-          c = ((uint32_t)nb8[1] << 24) | ((uint32_t)nb8[2] << 16) | ((uint32_t)nb8[3] << 8) | nb8[4];
-        } else {
-          f = a.nflag;
-          c = a.nctr0 + r;
-          if (!DECRYPT && s == 0u && q == 0u) {
-            nb8[0] = (uint8_t)f;
-            nb8[1] = (uint8_t)(c >> 24);
-            nb8[2] = (uint8_t)(c >> 16);
-            nb8[3] = (uint8_t)(c >> 8);
-            nb8[4] = (uint8_t)c;
-          }
-        }
-        n0 = 0x30303030u;                 // "0000"
-        n1 = 0x00303030u | (f << 24);     // "000" || flag
-        n2 = __builtin_bswap32(c);        // BE32 counter
-      }
-    }
+    gcm_nonce(a, r, !DECRYPT && s == 0u && q == 0u, n0, n1, n2);
 
     u32x4 acc = {0u, 0u, 0u, 0u};
     u32x4 ekj0 = {0u, 0u, 0u, 0u};
@@ -270,6 +278,104 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- wide decomposition
+// Few long records (the naive Alltoall's p peer blocks of 1 MiB, alltoall.c:795-834): a record's
+// X-sequence is cut from the END into chunks of C = 64*S X-blocks (chunk 0 may be shorter) and
+// every (record, chunk) is ONE wavefront.  At step k lane q owns X position base + 64k + q, so
+// each wave-instruction moves 1 KiB of contiguous record data, and the lane folds its blocks
+// into a Horner accumulator with multiplier H^64 (byte table of H^64 in LDS).  Lane q's last
+// block sits at end - 64 + q in every chunk, so its sum is weighted by
+//   wtab[i*64 + q] = H^{(nch-1-i)*C + 64 - q}        (host-built per (C, nch), cached)
+// with one generic multiply, XOR-reduced over the wave and written as the chunk's partial;
+// gcm_combine_kernel (pw = null) XORs the partials with E_K(J0) into the tag.
+template <bool DECRYPT>
+__global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
+  stage_copy(a.htab, 0u, 4096u);  // byte table of H^64
+  stage_rows(a.te0, kGcmRows);
+  __syncthreads();
+
+  const RoundKeys rk = a.rk;
+  const uint32_t lane = threadIdx.x & 63u;
+  const RowLanes rl = row_lanes(kGcmRows);
+  const GhashLane gl = ghash_lane();
+  const uint32_t nb = a.nb;
+  const int32_t nx = (int32_t)nb + 1;
+  const uint32_t rem = a.len - 16u * (nb ? nb - 1u : 0u);
+  const uint64_t cbits = (uint64_t)a.len * 8u;
+  const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
+  const int32_t C = 64 * (int32_t)a.S;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t units = a.nrec * a.nch;
+
+  for (uint32_t u = blockIdx.x * wpb + (threadIdx.x >> 6); u < units; u += gridDim.x * wpb) {
+    const uint32_t r = u / a.nch;
+    const uint32_t i = u - r * a.nch;
+    const int32_t base = nx - (int32_t)(a.nch - i) * C;  // position of step 0, lane 0 (may be < 0)
+    const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
+    uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
+    uint32_t n0, n1, n2;
+    gcm_nonce(a, r, !DECRYPT && i == 0u && lane == 0u, n0, n1, n2);
+
+    // (records of a wide batch always have full blocks: nb >= 64)
+    auto full_blk = [&](int32_t p) { return p >= 0 && p < (int32_t)nb && (p + 1 < (int32_t)nb || rem == 16u); };
+    auto prefetch = [&](uint32_t k) -> u32x4 {
+      const int32_t p = base + 64 * (int32_t)k + (int32_t)lane;
+      return ld_blk(in_rec + 16u * (uint32_t)(full_blk(p) ? p : 0));
+    };
+    CtrCache cc;
+    uint32_t cc_win = 0xffffffffu;
+    auto keystream = [&](uint32_t ctr) -> u32x4 {
+      const uint32_t w3 = __builtin_bswap32(ctr);
+      if ((ctr >> 8) != cc_win) {
+        ctr_cache_fill(rk, rl, n0, n1, n2, w3, cc);
+        cc_win = ctr >> 8;
+      }
+      uint32_t s0, s1, s2, s3;
+      aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
+      return u32x4{s0, s1, s2, s3};
+    };
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    auto consume = [&](uint32_t k, u32x4 v) {
+      const int32_t p = base + 64 * (int32_t)k + (int32_t)lane;
+      const u32x4 ks = keystream(2u + (uint32_t)p);  // block j = nonce || 2 + j
+      u32x4 x = {0u, 0u, 0u, 0u};
+      if (p >= 0 && p < (int32_t)nb) {
+        uint8_t* op = out_rec + 16u * (uint32_t)p;
+        if (full_blk(p)) {
+          const u32x4 o = v ^ ks;
+          st_blk(op, o);
+          x = DECRYPT ? v : o;
+        } else {
+          const u32x4 pp = load_partial(in_rec + 16u * (uint32_t)p, rem);
+          const u32x4 o = mask_bytes(pp ^ ks, rem);
+          store_partial(op, o, rem);
+          x = DECRYPT ? pp : o;
+        }
+      } else if (p == nx - 1) {
+        x = lenblk;
+      }
+      acc = gmul_byte(acc, gl) ^ x;
+    };
+    u32x4 va = prefetch(0), vb = prefetch(1);
+    uint32_t it = 0;
+    for (uint32_t k = 0; k < a.S; k += 2u) {
+      if (a.sched & 1u) rotate_prio(it++);
+      consume(k, va);
+      va = prefetch(k + 2u);
+      if (k + 1u < a.S) consume(k + 1u, vb);
+      vb = prefetch(k + 3u);
+    }
+    u32x4 f = gmul_generic(acc, a.wtab[(uint64_t)i * 64u + lane]);
+    if (i == 0u) {  // E_K(J0) joins the first chunk's partial
+      const u32x4 e = keystream(1u);
+      if (lane == 0u) f ^= e;
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) f ^= shfl_xor4(f, m);
+    if (lane == 0u) a.partial[u] = f;
+  }
+}
+
 struct GcmCombineArgs {
   const uint8_t* in;   // open: ct||tag records (for the received tag)
   uint8_t* out;        // seal: ct||tag records (tag written); open: pt records (zeroed on failure)
@@ -290,11 +396,11 @@ __global__ __launch_bounds__(64) void gcm_combine_kernel(GcmCombineArgs a) {
   for (uint32_t s = lane; s < a.nseg; s += 64u) {
     const u32x4 p = a.partial[(uint64_t)r * a.nseg + s];
     const uint32_t k = a.nseg - 1u - s;
-    y ^= (k == 0u) ? p : gmul_generic(p, a.pw[k]);
+    y ^= (k == 0u || !a.pw) ? p : gmul_generic(p, a.pw[k]);  // pw null: partials pre-weighted
   }
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) y ^= shfl_xor4(y, m);
-  y ^= a.ekj0[r];
+  if (a.ekj0) y ^= a.ekj0[r];  // null: E_K(J0) already inside the partials (wide)
   int ok = 1;
   if (!DECRYPT) {
     if (lane == 0) {

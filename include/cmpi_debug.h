@@ -27,7 +27,12 @@ void cmpi_debug_set_ctr_lds(int lds_bytes);
 void cmpi_debug_set_sched(int mode);
 /* Chunk bytes of the pipelined host path (*_host calls; 0 = default 8 MiB). */
 void cmpi_debug_set_host_chunk(size_t bytes);
-/* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}. */
+/* Wide GCM decomposition (one wavefront per 64*steps-block chunk of a record, for few long
+ * records): mode 0 automatic, 1 always when legal (host-keyed context, >= 64 data blocks),
+ * -1 never; steps per chunk (0 = automatic). */
+void cmpi_debug_force_wide(int mode, uint32_t steps);
+/* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}; a wide plan reports
+ * L = 64, nseg = chunks per record, G = X-blocks per chunk (64*steps). */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);
 
 #ifdef __cplusplus

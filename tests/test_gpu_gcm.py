@@ -23,8 +23,10 @@ KEY = bytes.fromhex("000102030405060708090a0b0c0d0e0f")
 @pytest.fixture(autouse=True)
 def _auto_plan():
     aead.force_plan(0, 0)
+    aead.force_wide(0, 0)
     yield
     aead.force_plan(0, 0)
+    aead.force_wide(0, 0)
 
 
 def gpu_seal(ctx, nonces: np.ndarray, pt: np.ndarray) -> np.ndarray:
@@ -170,6 +172,40 @@ def test_large_records_multisegment():
     assert not back[3].any() and np.array_equal(back[[0, 1, 2, 4, 5, 6, 7]], pt[[0, 1, 2, 4, 5, 6, 7]])
 
 
+@pytest.mark.parametrize("n,nrec,steps", [(1024, 3, 1), (1040, 2, 1), (4097, 3, 2), (65535, 2, 4), (100000, 3, 3),
+                                          (1 << 20, 2, 0), (64 * 16 * 5 - 16, 2, 5)])
+def test_wide_decomposition(n, nrec, steps):
+    """Wide plan (one wave per 64*steps-block chunk; chunk 0 ragged; lane-weighted partials):
+    bit-exact seal, round trip, forged record zero-filled, unaligned wire layout."""
+    aead.force_wide(1, steps)
+    ctx = aead.AeadCtx(KEY)
+    L, nch, G, r0 = aead.gcm_plan(ctx, n, nrec)
+    assert L == 64 and G % 64 == 0 and 1 <= r0 <= G and nch == -(-(n // 16 + (n % 16 > 0) + 1) // G)
+    pt = records(0x3100 + n, nrec, n)
+    nonces = random_nonces(0x3200 + n, nrec)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    assert np.array_equal(gpu_seal(ctx, nonces, pt), want), (L, nch, G, r0)
+    forged = want.copy()
+    forged[nrec - 1, n // 2] ^= 0x10
+    back, st = gpu_open(ctx, nonces, forged)
+    assert list(st) == [1] * (nrec - 1) + [0]
+    assert np.array_equal(back[: nrec - 1], pt[: nrec - 1]) and not back[nrec - 1].any()
+    # naive-collective wire layout (odd stride), in place of the dense one
+    stride = n + 28
+    wire = np.zeros((nrec, stride), np.uint8)
+    wire[:, :12] = nonces
+    wbuf = dev(wire)
+    ctx.seal_batch(wbuf[12:], dev(pt), wbuf, n, nrec, out_stride=stride, nonce_stride=stride)
+    assert np.array_equal(host(wbuf).reshape(nrec, stride)[:, 12:], want)
+
+
+def test_wide_auto_for_naive_alltoall_blocks():
+    """8 peer blocks of 1 MiB (BASELINE config 5 per rank) pick the wide plan automatically."""
+    ctx = aead.AeadCtx(KEY)
+    assert aead.gcm_plan(ctx, 1 << 20, 8)[0] == 64
+    assert aead.gcm_plan(ctx, 1024, 65536)[0] != 64
+
+
 def test_config2_full_batch_properties():
     """65 536 x 1 KiB (BASELINE config 2): seal->open round trip over the whole batch,
     every tag unique, and a seeded sample bit-exact against the oracle."""
@@ -302,6 +338,33 @@ def test_device_keyed_ctx_rejects_ctr():
     import torch
 
     torch.cuda.synchronize()  # the key-setup kernel is asynchronous
+
+
+@pytest.mark.parametrize("out_pad", [0, 28])
+def test_host_pipeline_pinned_in_and_out(out_pad):
+    """Registered host buffers on both sides move by flat DMA (device pitch = user stride) when
+    the output is dense; a gapped output (the wire layout's nonce between records) must keep
+    the caller's gap bytes."""
+    n, nrec = 1000, 257
+    pt = records(0x7171 + out_pad, nrec, n)
+    nonces = random_nonces(0x7172, nrec)
+    ctx = aead.AeadCtx(KEY)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    ostride = n + 16 + out_pad
+    out = np.full((nrec, ostride), 0x5A, np.uint8)
+    L = aead.N.lib()
+    assert L.cmpi_host_register(pt.ctypes.data, pt.nbytes) == 0
+    assert L.cmpi_host_register(out.ctypes.data, out.nbytes) == 0
+    try:
+        L.cmpi_debug_set_host_chunk(64 * 1024)
+        aead.N.check(L.cmpi_gcm_seal_host(ctx.handle, out.ctypes.data, ostride, pt.ctypes.data, n,
+                                          nonces.ctypes.data, 12, n, nrec))
+        assert np.array_equal(out[:, : n + 16], want)
+        assert (out[:, n + 16:] == 0x5A).all()
+    finally:
+        L.cmpi_debug_set_host_chunk(0)
+        L.cmpi_host_unregister(pt.ctypes.data)
+        L.cmpi_host_unregister(out.ctypes.data)
 
 
 @pytest.mark.parametrize("alg", ["aes-128-gcm", "aes-128-ocb"])
