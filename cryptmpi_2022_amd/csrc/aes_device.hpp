@@ -61,6 +61,19 @@ struct RoundKeys {
   uint32_t w[44];
 };
 
+// Folded round keys.  A round column is T0[a] ^ T1[b] ^ K ^ rotl16(T0[c] ^ T1[d]); written as
+// xor3(T0[a], T1[b], rotl16(xor3(T0[c], T1[d], rotl16(K)))) it is 3 VALU instead of 4 (rotl16
+// is an involution).  The wave-uniform rotl16(K) of rounds 1..9 (words 4..39) is computed once
+// by the host (kernel arguments) or the keysetup kernel: every AES routine below takes keys folded; words
+// 0..3 (whitening) and 40..43 (last round) stay as they are.
+__device__ __forceinline__ uint32_t srot16(uint32_t x) { return (x << 16) | (x >> 16); }
+__device__ __forceinline__ RoundKeys fold_keys(const RoundKeys& k) {
+  RoundKeys f = k;
+#pragma unroll
+  for (int i = 4; i < 40; ++i) f.w[i] = srot16(k.w[i]);
+  return f;
+}
+
 // Lane constants of a row image at `base` (multiple of 64 KiB): Te0/Td0 half and Te1/Td1 half.
 struct RowLanes {
   uint32_t l0, l1;
@@ -70,17 +83,17 @@ __device__ __forceinline__ RowLanes row_lanes(uint32_t base) {
   return RowLanes{l, l | 128u};
 }
 
-// One AES-128 encryption round (rounds 1..9) on state s, encryption row image.
+// One AES-128 encryption round (rounds 1..9) on state s, encryption row image; k* folded.
 __device__ __forceinline__ void enc_round(const RowLanes& L, uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
                                           uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   const uint32_t a0 = lds32(ra<0>(s0, L.l0)), a1 = lds32(ra<1>(s1, L.l1)), a2 = lds32(ra<2>(s2, L.l0)), a3 = lds32(ra<3>(s3, L.l1));
   const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l1)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l1));
   const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l1)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l1));
   const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l1)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l1));
-  s0 = xor3(a0, a1, k0) ^ rotl16(a2 ^ a3);
-  s1 = xor3(b0, b1, k1) ^ rotl16(b2 ^ b3);
-  s2 = xor3(c0, c1, k2) ^ rotl16(c2 ^ c3);
-  s3 = xor3(d0, d1, k3) ^ rotl16(d2 ^ d3);
+  s0 = xor3(a0, a1, rotl16(xor3(a2, a3, k0)));
+  s1 = xor3(b0, b1, rotl16(xor3(b2, b3, k1)));
+  s2 = xor3(c0, c1, rotl16(xor3(c2, c3, k2)));
+  s3 = xor3(d0, d1, rotl16(xor3(d2, d3, k3)));
 }
 
 // Last encryption round: S[x] = byte 1 of Te0[x]; gather byte 1 of the four lookups per column.
@@ -96,7 +109,7 @@ __device__ __forceinline__ void enc_last(const RowLanes& L, uint32_t& s0, uint32
   s3 = xor3(perm(d1, d0, 0x0c0c0501u), perm(d3, d2, 0x05010c0cu), k3);
 }
 
-// Full AES-128 encryption of (s0..s3); round keys wave-uniform (kernarg -> SGPRs).
+// Full AES-128 encryption of (s0..s3); round keys folded, wave-uniform (kernarg -> SGPRs).
 __device__ __forceinline__ void aes128_enc(const RoundKeys& k, const RowLanes& L, uint32_t& s0, uint32_t& s1,
                                            uint32_t& s2, uint32_t& s3) {
   s0 ^= k.w[0];
@@ -134,21 +147,22 @@ struct CtrCache {
   uint32_t q0, q1, q2, q3;  // round-2 columns without the term fed by round-1 column 0
 };
 
-// w0..w3: any counter block of the window (byte 3 of w3 is ignored).
+// w0..w3: any counter block of the window (byte 3 of w3 is ignored).  k folded (fold_keys):
+// the round-1/2 keys are unfolded here (once per window).
 __device__ __forceinline__ void ctr_cache_fill(const RoundKeys& k, const RowLanes& L, uint32_t w0, uint32_t w1,
                                                uint32_t w2, uint32_t w3, CtrCache& c) {
   const uint32_t t0 = w0 ^ k.w[0], t1 = w1 ^ k.w[1], t2 = w2 ^ k.w[2], t3 = w3 ^ k.w[3];
-  c.k0 = xor3(lds32(ra<0>(t0, L.l0)), lds32(ra<1>(t1, L.l1)), k.w[4]) ^ rotl16(lds32(ra<2>(t2, L.l0)));
-  const uint32_t r1 = xor3(lds32(ra<0>(t1, L.l0)), lds32(ra<1>(t2, L.l1)), k.w[5]) ^
+  c.k0 = xor3(lds32(ra<0>(t0, L.l0)), lds32(ra<1>(t1, L.l1)), srot16(k.w[4])) ^ rotl16(lds32(ra<2>(t2, L.l0)));
+  const uint32_t r1 = xor3(lds32(ra<0>(t1, L.l0)), lds32(ra<1>(t2, L.l1)), srot16(k.w[5])) ^
                       rotl16(lds32(ra<2>(t3, L.l0)) ^ lds32(ra<3>(t0, L.l1)));
-  const uint32_t r2 = xor3(lds32(ra<0>(t2, L.l0)), lds32(ra<1>(t3, L.l1)), k.w[6]) ^
+  const uint32_t r2 = xor3(lds32(ra<0>(t2, L.l0)), lds32(ra<1>(t3, L.l1)), srot16(k.w[6])) ^
                       rotl16(lds32(ra<2>(t0, L.l0)) ^ lds32(ra<3>(t1, L.l1)));
-  const uint32_t r3 = xor3(lds32(ra<0>(t3, L.l0)), lds32(ra<1>(t0, L.l1)), k.w[7]) ^
+  const uint32_t r3 = xor3(lds32(ra<0>(t3, L.l0)), lds32(ra<1>(t0, L.l1)), srot16(k.w[7])) ^
                       rotl16(lds32(ra<2>(t1, L.l0)) ^ lds32(ra<3>(t2, L.l1)));
-  c.q0 = xor3(lds32(ra<1>(r1, L.l1)), k.w[8], rotl16(lds32(ra<2>(r2, L.l0)) ^ lds32(ra<3>(r3, L.l1))));
-  c.q1 = xor3(lds32(ra<0>(r1, L.l0)), lds32(ra<1>(r2, L.l1)), k.w[9]) ^ rotl16(lds32(ra<2>(r3, L.l0)));
-  c.q2 = xor3(lds32(ra<0>(r2, L.l0)), lds32(ra<1>(r3, L.l1)), k.w[10]) ^ rotl16(lds32(ra<3>(r1, L.l1)));
-  c.q3 = xor3(lds32(ra<0>(r3, L.l0)), k.w[11], rotl16(lds32(ra<2>(r1, L.l0)) ^ lds32(ra<3>(r2, L.l1))));
+  c.q0 = xor3(lds32(ra<1>(r1, L.l1)), srot16(k.w[8]), rotl16(lds32(ra<2>(r2, L.l0)) ^ lds32(ra<3>(r3, L.l1))));
+  c.q1 = xor3(lds32(ra<0>(r1, L.l0)), lds32(ra<1>(r2, L.l1)), srot16(k.w[9])) ^ rotl16(lds32(ra<2>(r3, L.l0)));
+  c.q2 = xor3(lds32(ra<0>(r2, L.l0)), lds32(ra<1>(r3, L.l1)), srot16(k.w[10])) ^ rotl16(lds32(ra<3>(r1, L.l1)));
+  c.q3 = xor3(lds32(ra<0>(r3, L.l0)), srot16(k.w[11]), rotl16(lds32(ra<2>(r1, L.l0)) ^ lds32(ra<3>(r2, L.l1))));
 }
 
 // E_K(counter block) for a block of the cached window; w3 = its last word.
@@ -172,6 +186,7 @@ __device__ __forceinline__ uint32_t sb1(uint32_t w) { return (w >> 1) & 0x7f80u;
 __device__ __forceinline__ uint32_t sb2(uint32_t w) { return (w >> 9) & 0x7f80u; }
 __device__ __forceinline__ uint32_t sb3(uint32_t w) { return (w >> 17) & 0x7f80u; }
 
+// (k: the decryption key schedule, folded by fold_keys like the encryption one.)
 __device__ __forceinline__ void aes128_dec(const RoundKeys& k, const RowLanes& LD, uint32_t lbs, uint32_t& s0,
                                            uint32_t& s1, uint32_t& s2, uint32_t& s3) {
   s0 ^= k.w[0];
@@ -185,10 +200,10 @@ __device__ __forceinline__ void aes128_dec(const RoundKeys& k, const RowLanes& L
     const uint32_t b0 = lds32(ra<0>(s1, LD.l0)), b1 = lds32(ra<1>(s0, LD.l1)), b2 = lds32(ra<2>(s3, LD.l0)), b3 = lds32(ra<3>(s2, LD.l1));
     const uint32_t c0 = lds32(ra<0>(s2, LD.l0)), c1 = lds32(ra<1>(s1, LD.l1)), c2 = lds32(ra<2>(s0, LD.l0)), c3 = lds32(ra<3>(s3, LD.l1));
     const uint32_t d0 = lds32(ra<0>(s3, LD.l0)), d1 = lds32(ra<1>(s2, LD.l1)), d2 = lds32(ra<2>(s1, LD.l0)), d3 = lds32(ra<3>(s0, LD.l1));
-    s0 = xor3(a0, a1, k.w[4 * r + 0]) ^ rotl16(a2 ^ a3);
-    s1 = xor3(b0, b1, k.w[4 * r + 1]) ^ rotl16(b2 ^ b3);
-    s2 = xor3(c0, c1, k.w[4 * r + 2]) ^ rotl16(c2 ^ c3);
-    s3 = xor3(d0, d1, k.w[4 * r + 3]) ^ rotl16(d2 ^ d3);
+    s0 = xor3(a0, a1, rotl16(xor3(a2, a3, k.w[4 * r + 0])));  // k folded
+    s1 = xor3(b0, b1, rotl16(xor3(b2, b3, k.w[4 * r + 1])));
+    s2 = xor3(c0, c1, rotl16(xor3(c2, c3, k.w[4 * r + 2])));
+    s3 = xor3(d0, d1, rotl16(xor3(d2, d3, k.w[4 * r + 3])));
   }
   const uint32_t a0 = lds32(sb0(s0) | lbs), a1 = lds32(sb1(s3) | lbs), a2 = lds32(sb2(s2) | lbs), a3 = lds32(sb3(s1) | lbs);
   const uint32_t b0 = lds32(sb0(s1) | lbs), b1 = lds32(sb1(s0) | lbs), b2 = lds32(sb2(s3) | lbs), b3 = lds32(sb3(s2) | lbs);

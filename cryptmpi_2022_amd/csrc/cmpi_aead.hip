@@ -125,6 +125,14 @@ struct cmpi_ctx {
 
 namespace {
 
+// Kernel-argument round keys are passed folded (aes_device.hpp fold_keys): rounds 1..9 as
+// rotl16(K), so each AES column costs 3 VALU and the kernels keep them as plain kernargs.
+cmpi::dev::RoundKeys folded(const cmpi::dev::RoundKeys& k) {
+  cmpi::dev::RoundKeys f = k;
+  for (int i = 4; i < 40; ++i) f.w[i] = (k.w[i] << 16) | (k.w[i] >> 16);
+  return f;
+}
+
 int ensure_buf(void** p, size_t* cap, size_t need) {
   if (need <= *cap) return CMPI_OK;
   if (*p) (void)hipFree(*p);
@@ -160,6 +168,7 @@ struct GcmPlan {
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
+std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4/6
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
 std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
@@ -294,6 +303,12 @@ int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
 template <int L, bool DEC>
 int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
   auto fn = cmpi::dev::gcm_batch_kernel<L, DEC>;
+  switch (g_gcm_pf.load()) {
+    case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 3>; break;
+    case 4: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 4>; break;
+    case 6: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 6>; break;
+    default: break;
+  }
   if constexpr (!DEC) {
     switch (g_gcm_ablation.load()) {
       case 1: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 1>; break;
@@ -354,7 +369,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.ntab = reinterpret_cast<const u32x4*>(c->dt->ntab[0]);
   a.te0 = c->dt->te0;
   a.status = status;
-  a.rk = c->rk;
+  a.rk = folded(c->rk);
   a.rkp = c->dev_keys ? c->dt->keys : nullptr;
   a.nmode = ns.mode;
   a.nctr0 = ns.ctr0;
@@ -506,7 +521,7 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   oa.nrec = (uint32_t)nrec;
   oa.te0 = c->dt->te0;
   oa.off0 = d_off0;
-  oa.rk = c->rk;
+  oa.rk = folded(c->rk);
   {
     int rc0 = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ocb_offset_kernel), c->device, 65536);
     if (rc0) return rc0;
@@ -533,9 +548,9 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.ltab = reinterpret_cast<const u32x4*>(c->dt->ltab);
   a.off0 = d_off0;
   a.partial = d_part;
-  a.rk = c->rk;
+  a.rk = folded(c->rk);
   a.sched = (uint32_t)g_sched.load();
-  a.drk = c->drk;
+  a.drk = folded(c->drk);
   const size_t lds = DEC ? cmpi::dev::kOcbLdsOpen : cmpi::dev::kOcbLdsSeal;
   const uint32_t per_cu = DEC ? 1u : 2u;  // LDS-limited 1024-thread blocks per CU
   auto fn = cmpi::dev::ocb_batch_kernel<DEC>;
@@ -562,7 +577,7 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   f.partial = d_part;
   f.off0 = d_off0;
   f.status = st_arr;
-  f.rk = c->rk;
+  f.rk = folded(c->rk);
   {
     int rc1 = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ocb_final_kernel<DEC>), c->device, cmpi::dev::kOcbLdsSeal);
     if (rc1) return rc1;
@@ -630,9 +645,11 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const bool in_flat = in_pinned && (nrec == 1 || in_stride <= in_rec + 64);
   const bool out_flat = out_pinned && (nrec == 1 || out_stride == out_rec);
   const size_t ip = in_flat ? in_stride : up16(in_rec), op = out_flat ? out_stride : up16(out_rec);
+  const bool n_flat = (nrec == 1 || nonce_stride <= 64) && is_pinned(nonces);
+  const size_t npitch = n_flat ? nonce_stride : 16;
   const size_t per = std::max<size_t>(1, g_host_chunk.load() / std::max<size_t>(std::max(ip, op), 16));
   const size_t K = std::min(per, nrec);  // records per chunk
-  const size_t in_b = ip * K, out_b = op * K, n_b = 16 * K, st_b = up16(4 * K);
+  const size_t in_b = ip * K, out_b = op * K, n_b = up16(npitch * K), st_b = up16(4 * K);
   const size_t slot_b = in_b + out_b + n_b + st_b;
   if (P.cap < slot_b) {
     for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
@@ -692,7 +709,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     if (ci >= 2) HIP_TRY(hipEventSynchronize(P.in_ready[sl]));
     if (in_rec && !in_pinned)
       for (size_t i = 0; i < nr; ++i) memcpy(h.in + i * ip, in + (r0 + i) * in_stride, in_rec);
-    for (size_t i = 0; i < nr; ++i) memcpy(h.n + 16 * i, nonces + (r0 + i) * nonce_stride, 12);
+    if (!n_flat)
+      for (size_t i = 0; i < nr; ++i) memcpy(h.n + 16 * i, nonces + (r0 + i) * nonce_stride, 12);
     if (ci >= 2) HIP_TRY(hipStreamWaitEvent(P.s[0], P.slot_free[sl], 0));
     if (in_rec) {
       if (in_flat)
@@ -702,14 +720,17 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
       else
         HIP_TRY(hipMemcpyAsync(d.in, h.in, ip * nr, hipMemcpyHostToDevice, P.s[0]));
     }
-    HIP_TRY(hipMemcpyAsync(d.n, h.n, 16 * nr, hipMemcpyHostToDevice, P.s[0]));
+    if (n_flat)
+      HIP_TRY(hipMemcpyAsync(d.n, nonces + r0 * nonce_stride, (nr - 1) * npitch + 12, hipMemcpyHostToDevice, P.s[0]));
+    else
+      HIP_TRY(hipMemcpyAsync(d.n, h.n, 16 * nr, hipMemcpyHostToDevice, P.s[0]));
     if ((rc = step("H2D", ci))) break;
     HIP_TRY(hipEventRecord(P.in_ready[sl], P.s[0]));
     HIP_TRY(hipStreamWaitEvent(P.s[1], P.in_ready[sl], 0));
     if (OCB)
-      rc = ocb_batch<DEC>(c, d.out, op, d.in, ip, d.n, 16, len, nr, DEC ? d.st : nullptr, nullptr, P.s[1]);
+      rc = ocb_batch<DEC>(c, d.out, op, d.in, ip, d.n, npitch, len, nr, DEC ? d.st : nullptr, nullptr, P.s[1]);
     else
-      rc = gcm_batch<DEC>(c, d.out, op, d.in, ip, d.n, 16, len, nr, DEC ? d.st : nullptr, nullptr, P.s[1]);
+      rc = gcm_batch<DEC>(c, d.out, op, d.in, ip, d.n, npitch, len, nr, DEC ? d.st : nullptr, nullptr, P.s[1]);
     if (rc) break;
     if ((rc = step("kernel", ci))) break;
     HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
@@ -756,7 +777,7 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   a.ctr_hi = cmpi::be64(ctr);
   a.ctr_lo = cmpi::be64(ctr + 8);
   a.te0 = c->dt->te0;
-  a.rk = c->rk;
+  a.rk = folded(c->rk);
   a.sched = (uint32_t)g_sched.load();
   const uint64_t blocks = (a.nblk + 1023) / 1024;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 2));
@@ -854,7 +875,10 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
   memcpy(ht->te0, cmpi::kAes.te0, sizeof ht->te0);
   memcpy(ht->td0, cmpi::kAes.td0, sizeof ht->td0);
   for (int x = 0; x < 256; ++x) ht->isb[x] = cmpi::kAes.inv_sbox[x];
-  memcpy(ht->keys, c->rk.w, sizeof c->rk.w);
+  {
+    const cmpi::dev::RoundKeys fk = folded(c->rk);  // same convention as the keysetup kernel
+    memcpy(ht->keys, fk.w, sizeof fk.w);
+  }
   memcpy(ht->keys + 48, c->H.b, 16);
   if (alg == CMPI_AES_128_GCM) {
     const Blk H2 = cmpi::gf_mul(c->H, c->H), H3 = cmpi::gf_mul(H2, c->H), H4 = cmpi::gf_mul(H2, H2);
@@ -949,6 +973,8 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
   g_force_nseg.store(segments);
 }
 
+void cmpi_debug_set_gcm_prefetch(int slots) { g_gcm_pf.store(slots == 3 || slots == 4 || slots == 6 ? slots : 2); }
+
 void cmpi_debug_force_wide(int mode, uint32_t steps) {
   g_force_wide.store(mode > 0 ? 1 : (mode < 0 ? -1 : 0));
   g_force_S.store(steps);
@@ -997,7 +1023,7 @@ int cmpi_gcm_seal_batch_fresh(const cmpi_ctx* c, uint8_t* out, size_t out_stride
   na.nrec = nrec;
   na.base = const_cast<cmpi_ctx*>(c)->nctr.fetch_add(nrec);
   na.te0 = c->dt->te0;
-  na.rk = c->nrk;
+  na.rk = folded(c->nrk);
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::nonce_drbg_kernel), c->device, 65536);
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nrec + 1023) / 1024, (uint64_t)c->ncu));
@@ -1118,7 +1144,7 @@ int cmpi_ecb_encrypt(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t 
   a.out = out;
   a.nblk = nblocks;
   a.te0 = c->dt->te0;
-  a.rk = c->rk;
+  a.rk = folded(c->rk);
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 1023) / 1024, (uint64_t)c->ncu * 2));
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ecb_kernel), c->device, 65536);
   if (rc) return rc;
@@ -1134,7 +1160,7 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   if (dst->device != base->device) return fail(CMPI_EINVAL, "contexts on different devices");
   DeviceGuard dg(dst->device);
   cmpi::dev::KeysetupArgs a{};
-  a.base = base->rk;
+  a.base = folded(base->rk);
   memcpy(a.v, v, 16);
   a.mode = 1;
   a.te0 = dst->dt->te0;

@@ -68,6 +68,7 @@ template <bool XOR_IN>
 __global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
   stage_rows(a.te0, 0u);
   __syncthreads();
+  const RoundKeys& rk = a.rk;  // folded by the host
   const RowLanes rl = row_lanes(0u);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t phase = a.ctr_lo & 63u;        // counter(v) = (ctr & ~63) + v, j = v - phase
@@ -91,11 +92,11 @@ __global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
     ctr_words(a.ctr_hi, lo_base, v, w0, w1, w2, w3);
     const uint64_t key = ((a.ctr_lo & 0xc0u) + st * 64u) >> 8;  // wave-uniform
     if (key != win) {
-      ctr_cache_fill(a.rk, rl, w0, w1, w2, w3, cc);
+      ctr_cache_fill(rk, rl, w0, w1, w2, w3, cc);
       win = key;
     }
     uint32_t s0, s1, s2, s3;
-    aes128_enc_ctr(a.rk, rl, cc, w3, s0, s1, s2, s3);
+    aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
     if (v >= phase && v - phase < a.nblk) ctr_emit<XOR_IN>(a, v - phase, u32x4{s0, s1, s2, s3}, in_cur);
     in_cur = ctr_load<XOR_IN>(a, v + 64u, phase, nfull);
   }
@@ -113,10 +114,11 @@ __global__ __launch_bounds__(1024) void ecb_kernel(EcbArgs a) {
   stage_rows(a.te0, 0u);
   __syncthreads();
   const RowLanes lb = row_lanes(0u);
+  const RoundKeys& rk = a.rk;  // folded by the host
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.nblk; j += (uint64_t)gridDim.x * blockDim.x) {
     const u32x4 v = *reinterpret_cast<const u32x4a*>(a.in + 16u * j);
     uint32_t s0 = v[0], s1 = v[1], s2 = v[2], s3 = v[3];
-    aes128_enc(a.rk, lb, s0, s1, s2, s3);
+    aes128_enc(rk, lb, s0, s1, s2, s3);
     *reinterpret_cast<u32x4a*>(a.out + 16u * j) = u32x4{s0, s1, s2, s3};
   }
 }
@@ -142,10 +144,11 @@ __global__ __launch_bounds__(1024) void nonce_drbg_kernel(NonceArgs a) {
   stage_rows(a.te0, 0u);
   __syncthreads();
   const RowLanes rl = row_lanes(0u);
+  const RoundKeys& rk = a.rk;  // folded by the host
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.nrec; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t c = a.base + r;
     uint32_t s0 = __builtin_bswap32((uint32_t)(c >> 32)), s1 = __builtin_bswap32((uint32_t)c), s2 = 0u, s3 = 0u;
-    aes128_enc(a.rk, rl, s0, s1, s2, s3);
+    aes128_enc(rk, rl, s0, s1, s2, s3);
     u32a* o = reinterpret_cast<u32a*>(a.out + r * a.stride);
     o[0] = s0;
     o[1] = s1;

@@ -122,14 +122,14 @@ __host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return kGcmNib + (
 // ABL (timing ablation, wrong results): bit 0 = GHASH multiply skipped, bit 1 = AES skipped
 // (keystream = counter block), bit 2 = record data addressed as one coalesced stream per wave
 // (same bytes moved, dense layouts only).
-template <int L, bool DECRYPT, int ABL = 0>
+template <int L, bool DECRYPT, int ABL = 0, int PF = 2>
 __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   stage_copy(a.htab, 0u, 4096u);
   stage_rows(a.te0, kGcmRows);
   if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)L * 512u);
   __syncthreads();
 
-  const RoundKeys rk = load_round_keys(a.rk, a.rkp);
+  const RoundKeys rk = load_round_keys(a.rk, a.rkp);  // folded (host / keysetup kernel)
   const uint32_t lane = threadIdx.x & 63u;
   const RowLanes rl = row_lanes(kGcmRows);
   const GhashLane gl = ghash_lane();
@@ -216,16 +216,20 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       return u32x4{s0, s1, s2, s3};
     };
     const uint32_t Lu = (uint32_t)L;
-    // Two input buffers: slot u's block is reloaded with slot u+2L's as soon as u is consumed,
-    // so each load has a whole slot of AES in front of its use and no register copies.
-    u32x4 va = prefetch(q), vb = prefetch(q + Lu);
+    // PF input buffers: slot u's block is reloaded with slot u+PF*L's as soon as u is consumed,
+    // so each load has PF-1 slots of AES in front of its use and no register copies.
+    u32x4 v[PF];
+#pragma unroll
+    for (int d = 0; d < PF; ++d) v[d] = prefetch(q + (uint32_t)d * Lu);
     uint32_t it = 0;
-    for (uint32_t u = q; u < nslots; u += 2u * Lu) {
+    for (uint32_t u = q; u < nslots; u += (uint32_t)PF * Lu) {
       if (a.sched & 1u) rotate_prio(it++);
-      consume(u, keystream(u), va);
-      va = prefetch(u + 2u * Lu);
-      if (u + Lu < nslots) consume(u + Lu, keystream(u + Lu), vb);
-      vb = prefetch(u + 3u * Lu);
+#pragma unroll
+      for (int d = 0; d < PF; ++d) {
+        const uint32_t uu = u + (uint32_t)d * Lu;
+        if (d == 0 || uu < nslots) consume(uu, keystream(uu), v[d]);
+        v[d] = prefetch(uu + (uint32_t)PF * Lu);
+      }
     }
 
     // ---- weight the lane's Horner sum by H^w, w = nxs - (lane's last X slot)
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
   stage_rows(a.te0, kGcmRows);
   __syncthreads();
 
-  const RoundKeys rk = a.rk;
+  const RoundKeys rk = a.rk;  // folded by the host
   const uint32_t lane = threadIdx.x & 63u;
   const RowLanes rl = row_lanes(kGcmRows);
   const GhashLane gl = ghash_lane();

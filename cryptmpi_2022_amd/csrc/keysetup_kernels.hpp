@@ -3,7 +3,7 @@
 // CryptMPI 602 per-message sub-key K' = AES_K(V) (send.c:572-600, recv.c:549-576) is derived,
 // expanded and tabled without a host round trip, ordered on the caller's stream.
 //
-// Output layout = DevTables in cmpi_aead.hip: keys[0..43] round keys, keys[48..51] H;
+// Output layout = DevTables in cmpi_aead.hip: keys[0..43] round keys (folded), keys[48..51] H;
 // byte tables of H, H^2, H^4 ([v][p], 4096 x 16 B each) and nibble tables of H^1..H^4
 // (512 x 16 B each) — bit-identical to gf128_host.hpp's host builders.
 #pragma once
@@ -13,7 +13,7 @@ namespace cmpi {
 namespace dev {
 
 struct KeysetupArgs {
-  RoundKeys base;       // mode 1: keys of K (the master key) used to derive K' = AES_K(V)
+  RoundKeys base;       // mode 1: keys of K (the master key, folded) used to derive K' = AES_K(V)
   uint32_t v[4];        // mode 0: K' itself; mode 1: V
   uint32_t mode;
   const uint32_t* te0;  // Te0 (global)
@@ -64,10 +64,11 @@ __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
     }
     rk.w[i] = rk.w[i - 4] ^ t;
   }
+  const RoundKeys fk = fold_keys(rk);  // stored folded: the GCM kernels load them as they are
   uint32_t h0 = 0u, h1 = 0u, h2 = 0u, h3 = 0u;
-  aes128_enc(rk, rl, h0, h1, h2, h3);  // H = E_K'(0^128)
+  aes128_enc(fk, rl, h0, h1, h2, h3);  // H = E_K'(0^128)
   const u32x4 H = u32x4{h0, h1, h2, h3};
-  if (threadIdx.x < 44u) a.keys[threadIdx.x] = rk.w[threadIdx.x];
+  if (threadIdx.x < 44u) a.keys[threadIdx.x] = fk.w[threadIdx.x];
   if (threadIdx.x == 0) {
     a.keys[48] = h0;
     a.keys[49] = h1;

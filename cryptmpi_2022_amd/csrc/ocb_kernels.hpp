@@ -109,6 +109,7 @@ __global__ __launch_bounds__(1024, DECRYPT ? 4 : 8) void ocb_batch_kernel(OcbArg
 
   const uint32_t lane = threadIdx.x & 63u;
   const RowLanes rl = row_lanes(0u);
+  const RoundKeys& ek = DECRYPT ? a.drk : a.rk;  // folded by the host
   const uint32_t lbs = 65536u | ((lane & 31u) << 2);
   const uint32_t waves_per_block = blockDim.x >> 6;
   const uint32_t total_waves = gridDim.x * waves_per_block;
@@ -147,8 +148,8 @@ __global__ __launch_bounds__(1024, DECRYPT ? 4 : 8) void ocb_batch_kernel(OcbArg
         const u32x4 v = vcur;
         u32x4 x = v ^ off;
         uint32_t s0 = x[0], s1 = x[1], s2 = x[2], s3 = x[3];
-        if (DECRYPT) aes128_dec(a.drk, rl, lbs, s0, s1, s2, s3);
-        else aes128_enc(a.rk, rl, s0, s1, s2, s3);
+        if (DECRYPT) aes128_dec(ek, rl, lbs, s0, s1, s2, s3);
+        else aes128_enc(ek, rl, s0, s1, s2, s3);
         const u32x4 y = u32x4{s0, s1, s2, s3} ^ off;
         *reinterpret_cast<u32x4a*>(out_rec + boff) = y;
         csum ^= DECRYPT ? y : v;
@@ -185,6 +186,7 @@ __global__ __launch_bounds__(256) void ocb_final_kernel(OcbFinalArgs a) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.nrec) return;
   const RowLanes lb = row_lanes(0u);
+  const RoundKeys& rk = a.rk;  // folded by the host
   const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
   uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
   u32x4 csum = {0u, 0u, 0u, 0u};
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(256) void ocb_final_kernel(OcbFinalArgs a) {
   if (rem) {
     off ^= ocb_l(kOcbLSeal, 0u);  // Offset_* = Offset_m ^ L_*
     uint32_t p0 = off[0], p1 = off[1], p2 = off[2], p3 = off[3];
-    aes128_enc(a.rk, lb, p0, p1, p2, p3);  // Pad
+    aes128_enc(rk, lb, p0, p1, p2, p3);  // Pad
     const u32x4 pad = {p0, p1, p2, p3};
     const u32x4 v = load_partial(in_rec + 16u * a.m, rem);
     const u32x4 o = mask_bytes(v ^ pad, rem);
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(256) void ocb_final_kernel(OcbFinalArgs a) {
   }
   u32x4 t = csum ^ off ^ ocb_l(kOcbLSeal, 1u);
   uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
-  aes128_enc(a.rk, lb, t0, t1, t2, t3);
+  aes128_enc(rk, lb, t0, t1, t2, t3);
   const u32x4 tag = {t0, t1, t2, t3};
   if (!DECRYPT) {
     uint8_t* tp = out_rec + a.len;

@@ -27,6 +27,8 @@ void cmpi_debug_set_ctr_lds(int lds_bytes);
 void cmpi_debug_set_sched(int mode);
 /* Chunk bytes of the pipelined host path (*_host calls; 0 = default 8 MiB). */
 void cmpi_debug_set_host_chunk(size_t bytes);
+/* GCM lane-group kernel: input prefetch depth in slots (2, 3, 4 or 6; anything else = 2). */
+void cmpi_debug_set_gcm_prefetch(int slots);
 /* Wide GCM decomposition (one wavefront per 64*steps-block chunk of a record, for few long
  * records): mode 0 automatic, 1 always when legal (host-keyed context, >= 64 data blocks),
  * -1 never; steps per chunk (0 = automatic). */

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of one engine knob (a cmpi_debug_* setter taking an int) on bench workloads:
+HIP-event median of seal and open per knob value, one process.
+
+    python tools/ab_knob.py cmpi_debug_set_gcm_prefetch 2,3,4,6 gcm1k gcm4k
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from bench import Workload  # noqa: E402
+from cryptmpi_2022_amd import _native as N  # noqa: E402
+
+setter = getattr(N.lib(), sys.argv[1])
+values = [int(x) for x in sys.argv[2].split(",")]
+res = {}
+for wl in sys.argv[3:]:
+    w = Workload(wl, 0, seed=3)
+    t = {(v, op): [] for v in values for op in ("seal", "open")}
+    for rnd in range(7):
+        for v in values:
+            setter(v)
+            for op in ("seal", "open"):
+                fn = w.seal if op == "seal" else w.open
+                fn()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(4):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                t[(v, op)].append(e0.elapsed_time(e1) / 4)
+    ok = w.verify()
+    for (v, op), ts in t.items():
+        m = sorted(ts)[len(ts) // 2]
+        res[f"{wl}_{op}_{v}"] = {"ms": round(m, 4), "GiBps": round(w.n * w.nrec / (m * 1e-3) / 2**30, 1)}
+    res[f"{wl}_verified"] = ok
+    setter(values[0])
+    w.free()
+print(json.dumps(res, indent=0))
