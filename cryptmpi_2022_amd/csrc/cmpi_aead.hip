@@ -316,6 +316,7 @@ int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size
       case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 3>; break;
       case 4: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 4>; break;
       case 7: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 7>; break;
+      case 8: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 8>; break;
       default: break;
     }
   }
@@ -962,7 +963,7 @@ int cmpi_host_unregister(void* ptr) {
 
 void cmpi_debug_set_sched(int mode) { g_sched.store(mode & 7); }
 void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)8 << 20)); }
-void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 7); }
+void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 15); }
 
 void cmpi_debug_set_ctr_lds(int lds_bytes) {
   g_ctr_lds.store(lds_bytes >= 65536 && lds_bytes <= 163840 ? lds_bytes : 65536);

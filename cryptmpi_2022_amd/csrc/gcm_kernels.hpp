@@ -32,7 +32,7 @@ struct GcmArgs {
   uint32_t G;       // X-blocks per segment (all but the first)
   uint32_t r0;      // X-blocks in the first segment
   uint32_t ngroups; // nrec * nseg
-  const u32x4* htab;   // [v][p] byte table of H^L (global), 4096 entries
+  const u32x4* htab;   // [v][p] byte table of H^L (global), 4096 entries (wide kernel: H^64)
   const u32x4* ntab;   // nibble tables of H^1..H^L (global), L*512 entries (L > 1)
   const uint32_t* te0; // Te0 (global), 256 words
   u32x4* partial;      // nrec*nseg segment partials (nseg > 1)
@@ -128,6 +128,10 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   stage_rows(a.te0, kGcmRows);
   if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)L * 512u);
   __syncthreads();
+  if (ABL & 8) {  // prologue only (table staging cost)
+    if (threadIdx.x == 0 && a.nrec == 0xFFFFFFFFu) a.out[0] = (uint8_t)lds32(0u);
+    return;
+  }
 
   const RoundKeys rk = load_round_keys(a.rk, a.rkp);  // folded (host / keysetup kernel)
   const uint32_t lane = threadIdx.x & 63u;

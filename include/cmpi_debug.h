@@ -18,7 +18,7 @@ extern "C" {
  * (0 = automatic) for every subsequent launch in the process. */
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments);
 /* Timing ablation of the GCM seal kernel (results become WRONG): 0 full, 1 no GHASH multiply,
- * 2 no AES, 3 neither, 4 coalesced stand-in addressing, 7 = 3 + 4. */
+ * 2 no AES, 3 neither, 4 coalesced stand-in addressing, 7 = 3 + 4, 8 = table staging only. */
 void cmpi_debug_set_gcm_ablation(int mode);
 /* CTR kernel occupancy experiment: dynamic LDS bytes requested (65536..163840; more than
  * 80 KiB forces one 1024-thread block per CU). */
