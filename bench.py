@@ -241,6 +241,67 @@ def host_path_rate(device: int, n: int = 1024, nrec: int = 65536) -> dict:
     return res
 
 
+def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, warmup: int = 3) -> dict:
+    """BASELINE config 5 end to end, MPIR_Naive_Sec_Alltoall (alltoall.c:764-836) per rank:
+    seal the p peer blocks with fresh nonces into the wire layout nonce||ct||tag (one batched
+    call), exchange the wire blocks (RCCL all_to_all_single over xGMI; one rank: a device copy),
+    open the p received blocks (one batched call), on one stream.  Every rank runs this;
+    time = MAX over ranks; rate = plaintext bytes each rank sent / time."""
+    from cryptmpi_2022_amd import _native as N
+
+    p = pg.get_world_size() if pg is not None else 1
+    dev = torch.device("cuda", device)
+    g = torch.Generator(device=dev).manual_seed(4242 + (pg.get_rank() if pg is not None else 0))
+    send = torch.randint(0, 256, (p * n,), dtype=torch.uint8, device=dev, generator=g)
+    recv = torch.empty_like(send)
+    wire = torch.empty(p * (n + 28), dtype=torch.uint8, device=dev)
+    wire_in = torch.empty_like(wire)
+    status = torch.zeros(p, dtype=torch.int32, device=dev)
+    ctx = aead.AeadCtx(KEY, device=device)
+    ws_bytes = max(ctx.workspace_size(n, p), 16)
+    ws_seal = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    ws_open = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    L = N.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def one():
+        N.check(L.cmpi_naive_seal_blocks(ctx.handle, P(wire), P(send), n, p, P(ws_seal), st))
+        if pg is not None and p > 1:
+            pg.all_to_all_single(wire_in, wire)
+        else:
+            wire_in.copy_(wire)
+        N.check(L.cmpi_naive_open_blocks(ctx.handle, P(recv), P(wire_in), n, p, P(status), P(ws_open), st))
+
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize(dev)
+    ok = bool((status == 1).all())
+    if p == 1:
+        ok = ok and torch.equal(recv, send)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize(dev)
+    barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if pg is not None and p > 1:
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        pg.all_reduce(okt, op=pg.ReduceOp.MIN)
+        ok = bool(okt.item())
+    wall = float(t.item())
+    ctx.close()
+    return {"ranks": p, "block_bytes": n, "ms_per_call": round(wall / steps * 1e3, 4),
+            "GiBps_per_rank": round(p * n * steps / wall / GIB, 2),
+            "GiBps_all_ranks": round(p * p * n * steps / wall / GIB, 2),
+            "transport": "RCCL all_to_all_single (xGMI)" if p > 1 else "1 rank: device copy",
+            "all_blocks_authenticated": ok}
+
+
 def cpu_baseline(workload: str, seconds: float = 10.0) -> dict:
     """Rank-0 CPU baselines on a bounded sample of the same workload shape.
     primary ('port'): the oracle's C restatement (oracle/liboracle.so), all host threads;
@@ -438,6 +499,10 @@ def main() -> None:
         except Exception as e:
             extras["host_path_pcie"] = {"error": repr(e)}
         result["extras"] = extras
+    if not args.no_extras:  # config 5 end to end: a collective, so every rank runs it
+        a2a = alltoall_e2e(local, pg, barrier)
+        if rank == 0:
+            result.setdefault("extras", {})["alltoall_e2e"] = a2a
     if rank == 0:
         print(json.dumps(result))
     if pg is not None:

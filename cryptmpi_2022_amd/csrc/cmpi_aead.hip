@@ -92,6 +92,8 @@ struct HostPipe {
   uint8_t* buf = nullptr;   // device staging, 2 slots
   uint8_t* hbuf = nullptr;  // pinned host staging, 2 slots (pageable user buffers)
   size_t cap = 0;
+  int32_t* hst = nullptr;   // pinned per-record open status of the whole batch
+  size_t hst_cap = 0;
   bool init = false;
 };
 
@@ -666,7 +668,21 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
     P.cap = slot_b;
   }
-  std::vector<int32_t> hst(DEC ? nrec : 0);
+  if (DEC && P.hst_cap < nrec) {  // statuses land here by DMA, chunk by chunk
+    for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
+    if (P.hst) (void)hipHostFree(P.hst);
+    P.hst = nullptr;
+    P.hst_cap = 0;
+    const size_t n = std::max<size_t>(nrec, 4096);
+    if (hipHostMalloc((void**)&P.hst, 4 * n, hipHostMallocDefault) != hipSuccess)
+      return fail(CMPI_ENOMEM, "hipHostMalloc status failed");
+    P.hst_cap = n;
+  }
+  // Host-side waits only where the CPU touches a staging slot: packing pageable inputs (or
+  // non-flat nonces) into it, unpacking pageable outputs from it.  With pinned buffers the
+  // whole batch is enqueued at once and the three streams pipeline on events alone.
+  const bool cpu_pack = (in_rec && !in_pinned) || !n_flat;
+  const bool cpu_unpack = out_rec && !out_pinned;
   const size_t nchunks = (nrec + K - 1) / K;
   static const bool dbg_sync = getenv("CMPI_DEBUG_SYNC") != nullptr;  // diagnose: sync + check each step
   auto step = [&](const char* what, size_t ci) -> int {
@@ -694,9 +710,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
     HIP_TRY(hipEventSynchronize(P.slot_free[sl]));
     const auto h = layout(sl, P.hbuf);
-    if (out_rec && !out_pinned)
-      for (size_t i = 0; i < nr; ++i) memcpy(out + (r0 + i) * out_stride, h.out + i * op, out_rec);
-    if (DEC) memcpy(hst.data() + r0, h.st, 4 * nr);
+    for (size_t i = 0; i < nr; ++i) memcpy(out + (r0 + i) * out_stride, h.out + i * op, out_rec);
     return CMPI_OK;
   };
   int rc = CMPI_OK;
@@ -707,7 +721,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     const auto h = layout(sl, P.hbuf);
     // slot sl was last used by chunk ci-2: its H2D must have read the pinned inputs and its
     // outputs must have been unpacked (done at iteration ci-1) before we overwrite them
-    if (ci >= 2) HIP_TRY(hipEventSynchronize(P.in_ready[sl]));
+    if (ci >= 2 && cpu_pack) HIP_TRY(hipEventSynchronize(P.in_ready[sl]));
     if (in_rec && !in_pinned)
       for (size_t i = 0; i < nr; ++i) memcpy(h.in + i * ip, in + (r0 + i) * in_stride, in_rec);
     if (!n_flat)
@@ -744,18 +758,18 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
       else
         HIP_TRY(hipMemcpyAsync(h.out, d.out, op * nr, hipMemcpyDeviceToHost, P.s[2]));
     }
-    if (DEC) HIP_TRY(hipMemcpyAsync(h.st, d.st, 4 * nr, hipMemcpyDeviceToHost, P.s[2]));
+    if (DEC) HIP_TRY(hipMemcpyAsync(P.hst + r0, d.st, 4 * nr, hipMemcpyDeviceToHost, P.s[2]));
     if ((rc = step("D2H", ci))) break;
     HIP_TRY(hipEventRecord(P.slot_free[sl], P.s[2]));
-    if (ci >= 1 && (rc = unpack(ci - 1))) break;  // overlaps the GPU work of chunk ci
+    if (cpu_unpack && ci >= 1 && (rc = unpack(ci - 1))) break;  // overlaps the GPU work of chunk ci
   }
-  if (!rc) rc = unpack(nchunks - 1);
+  if (!rc && cpu_unpack) rc = unpack(nchunks - 1);
   for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
   if (rc) return rc;
   if (DEC) {
     size_t bad = 0;
-    for (size_t i = 0; i < nrec; ++i) bad += hst[i] == 0;
-    if (status) memcpy(status, hst.data(), 4 * nrec);
+    for (size_t i = 0; i < nrec; ++i) bad += P.hst[i] == 0;
+    if (status) memcpy(status, P.hst, 4 * nrec);
     if (bad) return fail(CMPI_EAUTH, "%zu of %zu records failed authentication", bad, nrec);
   }
   return CMPI_OK;
@@ -941,6 +955,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
     }
     if (P.buf) (void)hipFree(P.buf);
     if (P.hbuf) (void)hipHostFree(P.hbuf);
+    if (P.hst) (void)hipHostFree(P.hst);
   }
   if (c->dt) (void)hipFree(c->dt);
   memset(c->key, 0, 16);
