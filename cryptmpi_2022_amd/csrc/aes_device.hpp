@@ -52,8 +52,17 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 __device__ __forceinline__ uint32_t perm(uint32_t a, uint32_t b, uint32_t sel) { return __builtin_amdgcn_perm(a, b, sel); }
 
 // Row-image address of (byte r of s): byte0/2/3 from the lane constant lb, byte1 = s.byte[r].
+// Measured on gfx950 (tools/probe/valu_rate.hip, 8 waves/SIMD): v_perm / v_alignbit / shifts
+// issue at ~4.2 cycles per wave-instruction, v_bitop3 with VGPR operands at ~2.9 — so byte 1,
+// already in place, is masked in with one fast bitop3 ((s & 0xff00) | lb, mask in a VGPR).
+__device__ __forceinline__ uint32_t byte1_mask() {
+  uint32_t m;
+  asm("v_mov_b32 %0, 0xff00" : "=v"(m));  // a VGPR operand: SGPR / literal operands issue slower
+  return m;
+}
 template <int R>
 __device__ __forceinline__ uint32_t ra(uint32_t s, uint32_t lb) {
+  if constexpr (R == 1) return __builtin_amdgcn_bitop3_b32(s, byte1_mask(), lb, 0xEA);  // (s & m) | lb
   return perm(s, lb, 0x03020400u | ((uint32_t)R << 8));
 }
 
