@@ -112,9 +112,9 @@ struct cmpi_ctx {
   // per-G segment power tables, H^{kG}
   mutable std::mutex mu;
   mutable std::map<uint32_t, std::pair<u32x4*, uint32_t>> pw;
-  // wide decomposition: byte table of H^64 and per-(S, nch) lane/chunk weights (lazy)
+  // wide decomposition (lazy): byte table of H^64, nibble tables of H^(2^b), b = 0..6
   mutable u32x4* h64tab = nullptr;
-  mutable std::map<std::pair<uint32_t, uint32_t>, u32x4*> wtab;
+  mutable u32x4* wnib = nullptr;
   // internal scratch (partials, status) and staging for *_host
   mutable void* scratch = nullptr;
   mutable size_t scratch_cap = 0;
@@ -222,7 +222,7 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
 
 // workspace: partials [nrec][nseg], E_K(J0) [nrec], and for device-keyed contexts H^{kG} [nseg]
 size_t gcm_ws_bytes(const cmpi_ctx* c, const GcmPlan& p, size_t nrec) {
-  if (p.wide) return (size_t)nrec * p.nseg * 16;
+  if (p.wide) return (size_t)nrec * p.nseg * 16 + nrec * 16;
   if (p.nseg <= 1) return 0;
   return (size_t)nrec * p.nseg * 16 + nrec * 16 + (c->dev_keys ? (size_t)p.nseg * 16 : 0);
 }
@@ -242,38 +242,22 @@ int get_h64tab(const cmpi_ctx* c, const u32x4** out) {
   return CMPI_OK;
 }
 
-// Wide-chunk weights wtab[i*64 + q] = H^{(nch-1-i)*64S + 64 - q}, cached per (S, nch):
-// row nch-1 holds H^{64-q}; each earlier row is the next one times H^{64S} (byte-table multiply).
-int get_wtab(const cmpi_ctx* c, uint32_t S, uint32_t nch, const u32x4** out) {
+// Lane weights of the wide kernel: nibble tables of H^(2^b), b = 0..6 (7 x 8 KiB), once per ctx.
+int get_wnib(const cmpi_ctx* c, const u32x4** out) {
   std::lock_guard<std::mutex> lk(c->mu);
-  auto key = std::make_pair(S, nch);
-  auto it = c->wtab.find(key);
-  if (it != c->wtab.end()) {
-    *out = it->second;
-    return CMPI_OK;
-  }
-  std::vector<Blk> mt(4096), w((size_t)nch * 64);
-  cmpi::build_byte_table(cmpi::gf_pow(c->H, 64ull * S), mt.data());
-  auto mul_t = [&](const Blk& x) {
-    Blk z{};
-    for (int p = 0; p < 16; ++p) {
-      const Blk& e = mt[(size_t)x.b[p] * 16 + p];
-      for (int b = 0; b < 16; ++b) z.b[b] ^= e.b[b];
+  if (!c->wnib) {
+    std::vector<Blk> tab(7 * 512);
+    Blk p = c->H;
+    for (int b = 0; b < 7; ++b) {
+      cmpi::build_nibble_table(p, tab.data() + (size_t)b * 512);
+      p = cmpi::gf_mul(p, p);
     }
-    return z;
-  };
-  Blk hq = cmpi::gf_one();  // H^{64-q} for q = 63 down to 0
-  for (int q = 63; q >= 0; --q) {
-    hq = cmpi::gf_mul(hq, c->H);
-    w[(size_t)(nch - 1) * 64 + q] = hq;
+    u32x4* d = nullptr;
+    HIP_TRY(hipMalloc(&d, tab.size() * 16));
+    HIP_TRY(hipMemcpy(d, tab.data(), tab.size() * 16, hipMemcpyHostToDevice));
+    c->wnib = d;
   }
-  for (int64_t i = (int64_t)nch - 2; i >= 0; --i)
-    for (int q = 0; q < 64; ++q) w[(size_t)i * 64 + q] = mul_t(w[(size_t)(i + 1) * 64 + q]);
-  u32x4* d = nullptr;
-  HIP_TRY(hipMalloc(&d, w.size() * 16));
-  HIP_TRY(hipMemcpy(d, w.data(), w.size() * 16, hipMemcpyHostToDevice));
-  c->wtab[key] = d;
-  *out = d;
+  *out = c->wnib;
   return CMPI_OK;
 }
 
@@ -390,10 +374,13 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
       ws = (uint8_t*)c->scratch;
     }
     a.partial = reinterpret_cast<u32x4*>(ws);
+    a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
     a.S = p.S;
     a.nch = p.nseg;
+    const u32x4* pw = nullptr;
     int rc = get_h64tab(c, &a.htab);
-    if (!rc) rc = get_wtab(c, p.S, p.nseg, &a.wtab);
+    if (!rc) rc = get_wnib(c, &a.wtab);
+    if (!rc) rc = get_pw(c, p.G, p.nseg, &pw);
     if (rc) return rc;
     auto fn = cmpi::dev::gcm_wide_kernel<DEC>;
     const size_t lds = 2 * 65536;
@@ -413,10 +400,10 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     ca.nrec = (uint32_t)nrec;
     ca.nseg = p.nseg;
     ca.partial = a.partial;
-    ca.ekj0 = nullptr;  // inside chunk 0's partial
-    ca.pw = nullptr;    // partials are weighted in-kernel
+    ca.ekj0 = a.ekj0;
+    ca.pw = pw;  // chunk i weighted by H^{(nch-1-i)·64S}, as segments
     ca.status = status;
-    hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(64), 0, st, ca);
+    hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(cmpi::dev::kCombineThreads), 0, st, ca);
     HIP_TRY(hipGetLastError());
     return CMPI_OK;
   }
@@ -464,7 +451,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     ca.ekj0 = a.ekj0;
     ca.pw = pw;
     ca.status = status;
-    hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(64), 0, st, ca);
+    hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(cmpi::dev::kCombineThreads), 0, st, ca);
     HIP_TRY(hipGetLastError());
   }
   return CMPI_OK;
@@ -938,7 +925,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   // scratch and staging go back to the allocator.
   (void)hipDeviceSynchronize();
   for (auto& kv : c->pw) (void)hipFree(kv.second.first);
-  for (auto& kv : c->wtab) (void)hipFree(kv.second);
+  if (c->wnib) (void)hipFree(c->wnib);
   if (c->h64tab) (void)hipFree(c->h64tab);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->stage) (void)hipFree(c->stage);
