@@ -65,3 +65,13 @@ def test_two_rank_alltoall_in_process():
         got = host(out)[: p * n].reshape(p, n)
         for r in range(p):
             assert got[r].tobytes() == send[r][q].tobytes()
+
+
+@pytest.mark.parametrize("n", [4096, 1 << 20])
+def test_bench_alltoall_e2e_one_rank(n):
+    """bench.py's BASELINE config-5 timing path (seal -> exchange -> open) on one rank: runs,
+    every block authenticates and the rank gets its own plaintext back."""
+    import bench
+
+    res = bench.alltoall_e2e(0, None, lambda: None, n=n, steps=2, warmup=1)
+    assert res["ranks"] == 1 and res["all_blocks_authenticated"] and res["ms_per_call"] > 0

@@ -199,6 +199,27 @@ def test_wide_decomposition(n, nrec, steps):
     assert np.array_equal(host(wbuf).reshape(nrec, stride)[:, 12:], want)
 
 
+@pytest.mark.parametrize("nrec,segments", [(3, 0), (2, 700), (1, 2)])
+def test_lane_groups_many_segments(nrec, segments):
+    """1 MiB records on the lane-group plan (wide disabled): hundreds of segment partials per
+    record, combined by 256 threads per record with H^{kG} weights (more partials than threads)."""
+    n = 1 << 20
+    aead.force_wide(-1, 0)
+    aead.force_plan(4, segments)
+    ctx = aead.AeadCtx(KEY)
+    L, nseg, G, r0 = aead.gcm_plan(ctx, n, nrec)
+    assert L == 4 and (nseg == 2 if segments == 2 else nseg > 256)
+    pt = records(0x4100 + nrec, nrec, n)
+    nonces = random_nonces(0x4200 + nrec, nrec)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    assert np.array_equal(gpu_seal(ctx, nonces, pt), want), (L, nseg, G, r0)
+    forged = want.copy()
+    forged[0, 12345] ^= 2
+    back, st = gpu_open(ctx, nonces, forged)
+    assert st[0] == 0 and not back[0].any()
+    assert (st[1:] == 1).all() and np.array_equal(back[1:], pt[1:])
+
+
 def test_wide_auto_for_naive_alltoall_blocks():
     """8 peer blocks of 1 MiB (BASELINE config 5 per rank) pick the wide plan automatically."""
     ctx = aead.AeadCtx(KEY)
