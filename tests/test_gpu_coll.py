@@ -75,3 +75,70 @@ def test_bench_alltoall_e2e_one_rank(n):
 
     res = bench.alltoall_e2e(0, None, lambda: None, n=n, steps=2, warmup=1)
     assert res["ranks"] == 1 and res["all_blocks_authenticated"] and res["ms_per_call"] > 0
+
+
+def _coll_rank(rank: int, ws: int, port: int, q):
+    import os
+    import traceback
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        torch.cuda.set_device(0)  # one GPU box: both ranks share cuda:0, ciphertext moves on the host
+        ctx = aead.AeadCtx(KEY)
+        n = 3000
+        plain = lambda r, i: records(0xC011 + 16 * r + i, 1, n)[0]  # noqa: E731  block (rank r, index i)
+        dv = lambda a: torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).cuda()  # noqa: E731
+        res = {}
+        # alltoall: rank r sends block (r, i) to rank i
+        recv = torch.empty(ws * n, dtype=torch.uint8, device="cuda")
+        coll.alltoall(ctx, dv(np.stack([plain(rank, i) for i in range(ws)])), recv, n)
+        res["alltoall"] = np.array_equal(recv.cpu().numpy().reshape(ws, n), np.stack([plain(r, rank) for r in range(ws)]))
+        # allgather
+        recv = torch.empty(ws * n, dtype=torch.uint8, device="cuda")
+        coll.allgather(ctx, dv(plain(rank, 0)), recv, n)
+        res["allgather"] = np.array_equal(recv.cpu().numpy().reshape(ws, n), np.stack([plain(r, 0) for r in range(ws)]))
+        # gather to root 1
+        recv = torch.empty(ws * n, dtype=torch.uint8, device="cuda")
+        coll.gather(ctx, dv(plain(rank, 1)), recv, n, root=1)
+        res["gather"] = rank != 1 or np.array_equal(recv.cpu().numpy().reshape(ws, n), np.stack([plain(r, 1) for r in range(ws)]))
+        # scatter from root 0: rank i gets block (0, i)
+        recv = torch.empty(n, dtype=torch.uint8, device="cuda")
+        coll.scatter(ctx, dv(np.stack([plain(0, i) for i in range(ws)])) if rank == 0 else None, recv, n, root=0)
+        res["scatter"] = np.array_equal(recv.cpu().numpy(), plain(0, rank))
+        # bcast from root 1
+        buf = dv(plain(1, 7)) if rank == 1 else torch.zeros(n, dtype=torch.uint8, device="cuda")
+        coll.bcast(ctx, buf, n, root=1)
+        res["bcast"] = np.array_equal(buf.cpu().numpy(), plain(1, 7))
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+def test_naive_collectives_two_processes():
+    """The five naive secure collectives end to end across two processes (gloo host transport of
+    the wire blocks, one GPU shared by both ranks): every rank gets the reference semantics'
+    plaintext back, every block authenticated."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    procs = [ctxm.Process(target=_coll_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=150) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert isinstance(out[r], dict), out[r]
+        assert all(out[r].values()), (r, out[r])
