@@ -81,7 +81,23 @@ struct DevTables {
   uint8_t htab[3][kByteTab];     // byte tables for H^1, H^2, H^4
   uint8_t ntab[kNibTables][kNibTab];
   uint8_t ltab[66][16];          // OCB: L_*, L_$, L_0..L_63
+  // device-keyed (602 sub-key) contexts: written by gcm_keysetup_kernel / gcm_tables_kernel
+  uint8_t sqtab[kByteTab];       // squaring map byte table (key independent, from the host)
+  uint8_t h2pow[32][16];         // H^(2^i)
+  uint8_t chains[8][128][16];    // basis chains of H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
+  uint8_t h64[kByteTab];         // byte table of H^64 (wide plan)
+  uint8_t wnib[7][kNibTab];      // nibble tables of H^(2^b), b < 7 (wide plan)
 };
+
+// The squaring-map table, built once per process.
+const std::vector<Blk>& sq_table() {
+  static const std::vector<Blk> t = [] {
+    std::vector<Blk> v(4096);
+    cmpi::build_sq_table(v.data());
+    return v;
+  }();
+  return t;
+}
 
 }  // namespace
 
@@ -199,11 +215,12 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   // records: the naive collectives' p peer blocks).  Host-keyed contexts only (the chunk
   // weights are built from H on the host); records need >= 64 data blocks.
   const int fw = g_force_wide.load();
-  const bool wide_ok = !c->dev_keys && p.nb >= 64;
+  const bool wide_ok = p.nb >= 64;
   if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target && nx >= 1024))) {
     uint64_t S = g_force_S.load();
     if (!S) S = std::max<uint64_t>(4, (uint64_t)nrec * nx / (64ull * c->ncu * (kGcmThreads / 64)));
     S = std::min<uint64_t>(S, (nx + 63) / 64);
+    if (c->dev_keys) S = (uint64_t)1 << (63 - __builtin_clzll(S));  // chunk weights from H^(2^i)
     p.wide = true;
     p.S = (uint32_t)S;
     p.L = 64;
@@ -213,6 +230,8 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     return p;
   }
   uint64_t G = (nx + nseg - 1) / nseg;
+  // device-keyed contexts weight segment partials by products of H^(2^i) (no host H): G = 2^g
+  if (c->dev_keys && nseg > 1 && G > 1) G = (uint64_t)1 << (64 - __builtin_clzll(G - 1));
   nseg = (nx + G - 1) / G;
   p.G = (uint32_t)G;
   p.nseg = (uint32_t)nseg;
@@ -224,11 +243,15 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
 size_t gcm_ws_bytes(const cmpi_ctx* c, const GcmPlan& p, size_t nrec) {
   if (p.wide) return (size_t)nrec * p.nseg * 16 + nrec * 16;
   if (p.nseg <= 1) return 0;
-  return (size_t)nrec * p.nseg * 16 + nrec * 16 + (c->dev_keys ? (size_t)p.nseg * 16 : 0);
+  return (size_t)nrec * p.nseg * 16 + nrec * 16;
 }
 
 // Byte table of H^64 (the wide kernel's Horner multiplier), built once per context.
 int get_h64tab(const cmpi_ctx* c, const u32x4** out) {
+  if (c->dev_keys) {  // built on the device by gcm_tables_kernel
+    *out = reinterpret_cast<const u32x4*>(c->dt->h64);
+    return CMPI_OK;
+  }
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->h64tab) {
     std::vector<Blk> tab(4096);
@@ -244,6 +267,10 @@ int get_h64tab(const cmpi_ctx* c, const u32x4** out) {
 
 // Lane weights of the wide kernel: nibble tables of H^(2^b), b = 0..6 (7 x 8 KiB), once per ctx.
 int get_wnib(const cmpi_ctx* c, const u32x4** out) {
+  if (c->dev_keys) {
+    *out = reinterpret_cast<const u32x4*>(c->dt->wnib[0]);
+    return CMPI_OK;
+  }
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->wnib) {
     std::vector<Blk> tab(7 * 512);
@@ -380,7 +407,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     const u32x4* pw = nullptr;
     int rc = get_h64tab(c, &a.htab);
     if (!rc) rc = get_wnib(c, &a.wtab);
-    if (!rc) rc = get_pw(c, p.G, p.nseg, &pw);
+    if (!rc && !c->dev_keys) rc = get_pw(c, p.G, p.nseg, &pw);
     if (rc) return rc;
     auto fn = cmpi::dev::gcm_wide_kernel<DEC>;
     const size_t lds = 2 * 65536;
@@ -402,6 +429,8 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     ca.partial = a.partial;
     ca.ekj0 = a.ekj0;
     ca.pw = pw;  // chunk i weighted by H^{(nch-1-i)·64S}, as segments
+    ca.h2pow = reinterpret_cast<const u32x4*>(c->dt->h2pow[0]);
+    ca.glog = (uint32_t)__builtin_ctz(p.G);  // dev_keys: G = 64S is a power of two
     ca.status = status;
     hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(cmpi::dev::kCombineThreads), 0, st, ca);
     HIP_TRY(hipGetLastError());
@@ -417,12 +446,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
     a.partial = reinterpret_cast<u32x4*>(ws);
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
-    if (c->dev_keys) {  // H is only on the device: build the combine weights there, in order
-      u32x4* d_pw = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16 + nrec * 16);
-      hipLaunchKernelGGL(cmpi::dev::gcm_powers_kernel, dim3(1), dim3(64), 0, st, c->dt->keys, p.G, p.nseg, d_pw);
-      HIP_TRY(hipGetLastError());
-      pw = d_pw;
-    } else {
+    if (!c->dev_keys) {  // device-keyed: weights from H^(2^i) in the combine (G = 2^g)
       int rc = get_pw(c, p.G, p.nseg, &pw);
       if (rc) return rc;
     }
@@ -450,6 +474,8 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     ca.partial = a.partial;
     ca.ekj0 = a.ekj0;
     ca.pw = pw;
+    ca.h2pow = reinterpret_cast<const u32x4*>(c->dt->h2pow[0]);
+    ca.glog = (uint32_t)__builtin_ctz(p.G);
     ca.status = status;
     hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(cmpi::dev::kCombineThreads), 0, st, ca);
     HIP_TRY(hipGetLastError());
@@ -882,6 +908,14 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
     memcpy(ht->keys, fk.w, sizeof fk.w);
   }
   memcpy(ht->keys + 48, c->H.b, 16);
+  memcpy(ht->sqtab, sq_table().data(), sizeof ht->sqtab);
+  {
+    Blk p = c->H;
+    for (int i = 0; i < 32; ++i) {
+      memcpy(ht->h2pow[i], p.b, 16);
+      p = cmpi::gf_mul(p, p);
+    }
+  }
   if (alg == CMPI_AES_128_GCM) {
     const Blk H2 = cmpi::gf_mul(c->H, c->H), H3 = cmpi::gf_mul(H2, c->H), H4 = cmpi::gf_mul(H2, H2);
     cmpi::build_byte_table(c->H, reinterpret_cast<Blk*>(ht->htab[0]));
@@ -1167,15 +1201,25 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   memcpy(a.v, v, 16);
   a.mode = 1;
   a.te0 = dst->dt->te0;
+  a.sqtab = reinterpret_cast<const u32x4*>(dst->dt->sqtab);
   a.keys = dst->dt->keys;
-  a.htab = reinterpret_cast<u32x4*>(dst->dt->htab[0]);
-  a.ntab = reinterpret_cast<u32x4*>(dst->dt->ntab[0]);
+  a.h2pow = reinterpret_cast<u32x4*>(dst->dt->h2pow[0]);
+  a.chains = reinterpret_cast<u32x4*>(dst->dt->chains[0]);
+  cmpi::dev::TablesArgs ta{};
+  ta.chains = a.chains;
+  ta.htab = reinterpret_cast<u32x4*>(dst->dt->htab[0]);
+  ta.h64 = reinterpret_cast<u32x4*>(dst->dt->h64);
+  ta.ntab = reinterpret_cast<u32x4*>(dst->dt->ntab[0]);
+  ta.wnib = reinterpret_cast<u32x4*>(dst->dt->wnib[0]);
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_keysetup_kernel), dst->device, cmpi::dev::kKsLds);
   if (rc) return rc;
   {
     std::lock_guard<std::mutex> lk(dst->mu);
     for (auto& kv : dst->pw) (void)hipFree(kv.second.first);
     dst->pw.clear();
+    if (dst->h64tab) (void)hipFree(dst->h64tab);
+    if (dst->wnib) (void)hipFree(dst->wnib);
+    dst->h64tab = dst->wnib = nullptr;
     dst->dev_keys = true;
     memset(dst->key, 0, 16);
     memset(&dst->rk, 0, sizeof dst->rk);
@@ -1183,6 +1227,9 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
     memset(&dst->H, 0, sizeof dst->H);
   }
   hipLaunchKernelGGL(cmpi::dev::gcm_keysetup_kernel, dim3(1), dim3(256), cmpi::dev::kKsLds, (hipStream_t)stream, a);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(cmpi::dev::gcm_tables_kernel, dim3((cmpi::dev::kTabEntries + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, ta);
   HIP_TRY(hipGetLastError());
   return CMPI_OK;
 }

@@ -305,7 +305,7 @@ template <bool DECRYPT>
 __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
   stage_rows(a.te0, kGcmRows);
 
-  const RoundKeys rk = a.rk;  // folded by the host
+  const RoundKeys rk = load_round_keys(a.rk, a.rkp);  // folded (host / keysetup kernel)
   const uint32_t lane = threadIdx.x & 63u;
   const RowLanes rl = row_lanes(kGcmRows);
   const GhashLane gl = ghash_lane();
@@ -413,7 +413,9 @@ struct GcmCombineArgs {
   uint32_t len, nb, nrec, nseg;
   const u32x4* partial;  // nrec*nseg
   const u32x4* ekj0;     // nrec
-  const u32x4* pw;       // pw[k] = H^{k*G}, k < nseg
+  const u32x4* pw;       // pw[k] = H^{k*G}, k < nseg (host-keyed contexts), or null and:
+  const u32x4* h2pow;    // H^(2^i), i < 32, with G = 2^glog (device-keyed contexts)
+  uint32_t glog;
   int32_t* status;
 };
 
@@ -430,7 +432,14 @@ __global__ __launch_bounds__(256) void gcm_combine_kernel(GcmCombineArgs a) {
   for (uint32_t s = t; s < a.nseg; s += blockDim.x) {
     const u32x4 p = a.partial[(uint64_t)r * a.nseg + s];
     const uint32_t k = a.nseg - 1u - s;
-    y ^= (k == 0u || !a.pw) ? p : gmul_generic32(p, a.pw[k]);  // pw null: partials pre-weighted
+    if (a.pw) {
+      y ^= k == 0u ? p : gmul_generic32(p, a.pw[k]);
+    } else {  // H^{k·2^glog} = product of H^(2^(glog + j)) over the set bits j of k
+      u32x4 q = p;
+      for (uint32_t m = k, j = a.glog; m; m >>= 1, ++j)
+        if (m & 1u) q = gmul_generic32(q, a.h2pow[j]);
+      y ^= q;
+    }
   }
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) y ^= shfl_xor4(y, m);

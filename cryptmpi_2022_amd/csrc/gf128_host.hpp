@@ -81,6 +81,26 @@ inline void build_byte_table(const Blk& P, Blk* tab) {
   }
 }
 
+// Byte table of the squaring map X -> X^2 (GF(2)-linear in characteristic 2), same [v][p]
+// layout as build_byte_table: tab[v*16 + p] = (block with byte p = v)^2.  Key independent.
+inline void build_sq_table(Blk* tab) {
+  for (int p = 0; p < 16; ++p) {
+    Blk basis[8];
+    for (int k = 0; k < 8; ++k) {
+      Blk e{};
+      e.b[p] = (uint8_t)(1u << k);
+      basis[k] = gf_mul(e, e);
+    }
+    for (int v = 0; v < 256; ++v) {
+      Blk acc{};
+      for (int k = 0; k < 8; ++k)
+        if (v & (1 << k))
+          for (int i = 0; i < 16; ++i) acc.b[i] ^= basis[k].b[i];
+      tab[v * 16 + p] = acc;
+    }
+  }
+}
+
 // Nibble-position table: tab[(2p)*16 + v] = (byte p = v<<4)·P, tab[(2p+1)*16 + v] = (byte p = v)·P.
 // 32 × 16 × 16 B = 8 KiB.
 inline void build_nibble_table(const Blk& P, Blk* tab) {

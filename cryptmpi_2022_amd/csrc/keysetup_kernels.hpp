@@ -3,9 +3,10 @@
 // CryptMPI 602 per-message sub-key K' = AES_K(V) (send.c:572-600, recv.c:549-576) is derived,
 // expanded and tabled without a host round trip, ordered on the caller's stream.
 //
-// Output layout = DevTables in cmpi_aead.hip: keys[0..43] round keys (folded), keys[48..51] H;
-// byte tables of H, H^2, H^4 ([v][p], 4096 x 16 B each) and nibble tables of H^1..H^4
-// (512 x 16 B each) — bit-identical to gf128_host.hpp's host builders.
+// Output layout = DevTables in cmpi_aead.hip: keys[0..43] round keys (folded), keys[48..51] H,
+// H^(2^i), basis chains; then gcm_tables_kernel expands byte tables of H, H^2, H^4, H^64
+// ([v][p], 4096 x 16 B each) and nibble tables of H^1..H^4 and H^(2^b) (512 x 16 B each) —
+// bit-identical to gf128_host.hpp's host builders.  Two launches, ~10 us in all.
 #pragma once
 #include "aes_device.hpp"
 
@@ -17,9 +18,10 @@ struct KeysetupArgs {
   uint32_t v[4];        // mode 0: K' itself; mode 1: V
   uint32_t mode;
   const uint32_t* te0;  // Te0 (global)
-  uint32_t* keys;       // out: [0..43] round keys of K', [48..51] H = E_K'(0)
-  u32x4* htab;          // out: 3 byte tables (H, H^2, H^4)
-  u32x4* ntab;          // out: 4 nibble tables (H^1..H^4)
+  const u32x4* sqtab;   // byte table of the squaring map X -> X^2 (key independent)
+  uint32_t* keys;       // out: [0..43] round keys of K' (folded), [48..51] H = E_K'(0)
+  u32x4* h2pow;         // out: H^(2^i), i < 32
+  u32x4* chains;        // out: basis chains P·x^i (i < 128) of P = H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
 };
 
 // GCM-order field element as (hi, lo) big-endian halves of its 16 memory bytes.
@@ -32,17 +34,27 @@ __device__ __forceinline__ u32x4 gf_join(uint64_t h, uint64_t l) {
                __builtin_bswap32((uint32_t)(l >> 32)), __builtin_bswap32((uint32_t)l)};
 }
 
-// LDS: AES row image @0 (64 KiB), basis chains Q_j[i] = P_j · x^i (j = 0..3 for H^1..H^4,
-// i = 0..127) @64K (8 KiB), S-box bytes @72K (256 words).
-constexpr uint32_t kKsBasis = 65536u;
-constexpr uint32_t kKsSbox = 73728u;
-constexpr uint32_t kKsLds = 74752u;
+// The 8 chained multipliers: index -> exponent of H.
+__host__ __device__ constexpr uint32_t ks_chain_exp(uint32_t j) {
+  return j == 0 ? 1u : j == 1 ? 2u : j == 2 ? 3u : j == 3 ? 4u : j == 4 ? 8u : j == 5 ? 16u : j == 6 ? 32u : 64u;
+}
 
+// LDS (dynamic only: offsets are addresses): squaring byte table @0 (64 KiB, read by
+// gmul_byte), AES row image @64K (64 KiB), S-box bytes @128K (256 words), H^(2^i) i < 7 after.
+constexpr uint32_t kKsRows = 65536u;
+constexpr uint32_t kKsSbox = 131072u;
+constexpr uint32_t kKsPow = kKsSbox + 1024u;
+constexpr uint32_t kKsLds = kKsPow + 8u * 16u;
+
+// One workgroup: key schedule of K' (= AES_K(V) in mode 1), H = E_K'(0), H^(2^i) by 31 table
+// squarings (the squaring map is GF(2)-linear: 16 LDS lookups each, no 128-step shift chain),
+// H^3 by one generic multiply, and the basis chains the table kernel expands.
 __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
-  stage_rows(a.te0, 0u);
+  stage_copy(a.sqtab, 0u, 4096u);
+  stage_rows(a.te0, kKsRows);
   for (uint32_t x = threadIdx.x; x < 256u; x += blockDim.x) lds_st32(kKsSbox + 4u * x, (a.te0[x] >> 8) & 0xffu);
   __syncthreads();
-  const RowLanes rl = row_lanes(0u);
+  const RowLanes rl = row_lanes(kKsRows);
   // every lane computes the (tiny) key schedule redundantly: no broadcast needed
   uint32_t k0 = a.v[0], k1 = a.v[1], k2 = a.v[2], k3 = a.v[3];
   if (a.mode == 1u) aes128_enc(a.base, rl, k0, k1, k2, k3);  // K' = AES_K(V)
@@ -75,55 +87,76 @@ __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
     a.keys[50] = h2;
     a.keys[51] = h3;
   }
-  // basis chains: lane j < 4 walks P_j = H^(j+1) through P_j · x^i, i = 0..127
-  if (threadIdx.x < 4u) {
-    u32x4 P = H;
-    for (uint32_t j = 0; j < threadIdx.x; ++j) P = gmul_generic(P, H);
+  // H^(2^i) by squaring (every lane of wave 0 redundantly; lane 0 stores)
+  if (threadIdx.x < 64u) {
+    const GhashLane gl = ghash_lane();
+    u32x4 p = H;
+    for (uint32_t i = 0; i < 32u; ++i) {
+      if (threadIdx.x == 0) {
+        a.h2pow[i] = p;
+        if (i < 7u) lds_st128(kKsPow + 16u * i, p);  // the chained multipliers H^(2^i), i < 7
+      }
+      p = gmul_byte(p, gl);  // p^2
+    }
+  }
+  __syncthreads();
+  // basis chains: lane j < 8 walks P_j through P_j · x^i, i = 0..127
+  if (threadIdx.x < 8u) {
+    const uint32_t j = threadIdx.x;
+    const u32x4 P = j == 2 ? gmul_generic32(lds128(kKsPow + 16u), lds128(kKsPow))  // H^3
+                           : lds128(kKsPow + 16u * (j < 2u ? j : j - 1u));       // H, H^2, H^4 .. H^64
     uint64_t ph, pl;
     gf_split(P, ph, pl);
     for (uint32_t i = 0; i < 128u; ++i) {
-      lds_st128(kKsBasis + (threadIdx.x * 128u + i) * 16u, gf_join(ph, pl));
+      a.chains[j * 128u + i] = gf_join(ph, pl);
       const uint64_t lsb = 0 - (pl & 1u);
       pl = (pl >> 1) | (ph << 63);
       ph = (ph >> 1) ^ (0xE100000000000000ULL & lsb);
     }
   }
-  __syncthreads();
-  // byte tables: entry (v, p) of P = XOR over set bits k of v of P · x^(8p + 7 - k)
-  const uint32_t bsel[3] = {0u, 1u, 3u};  // H, H^2, H^4
-  for (uint32_t e = threadIdx.x; e < 3u * 4096u; e += blockDim.x) {
-    const uint32_t t = e >> 12, v = (e >> 4) & 255u, p = e & 15u;
-    u32x4 acc = {0u, 0u, 0u, 0u};
-    for (uint32_t k = 0; k < 8u; ++k)
-      if (v & (1u << k)) acc ^= lds128(kKsBasis + (bsel[t] * 128u + 8u * p + 7u - k) * 16u);
-    a.htab[e] = acc;
-  }
-  // nibble tables: entry (2p + half, v): half 0 = byte p holds v << 4, half 1 = byte p holds v
-  for (uint32_t e = threadIdx.x; e < 4u * 512u; e += blockDim.x) {
-    const uint32_t t = e >> 9, row = (e >> 4) & 31u, v = e & 15u;
-    const uint32_t p = row >> 1, shift = (row & 1u) ? 0u : 4u;
-    u32x4 acc = {0u, 0u, 0u, 0u};
-    for (uint32_t k = 0; k < 4u; ++k)
-      if (v & (1u << k)) acc ^= lds128(kKsBasis + (t * 128u + 8u * p + 7u - (k + shift)) * 16u);
-    a.ntab[e] = acc;
-  }
 }
 
-// pw[k] = H^(k*G), k < n (multi-segment GCM combine weights) for a device-keyed context.
-__global__ __launch_bounds__(64) void gcm_powers_kernel(const uint32_t* keys, uint32_t G, uint32_t n, u32x4* pw) {
-  const u32x4 H = u32x4{keys[48], keys[49], keys[50], keys[51]};
-  for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
-    // square-and-multiply over the exponent k*G
-    uint64_t e = (uint64_t)k * G;
-    u32x4 r = {0x80u, 0u, 0u, 0u};  // 1 = x^0 (byte 0 bit 7)
-    u32x4 b = H;
-    while (e) {
-      if (e & 1u) r = gmul_generic(r, b);
-      b = gmul_generic(b, b);
-      e >>= 1;
-    }
-    pw[k] = r;
+// Table expansion, one entry per thread (grid over every entry): entry (v, p) of a byte table
+// of P = XOR over set bits k of v of P · x^(8p + 7 - k); nibble entry (2p + h, v) likewise over
+// the 4 bits of v at x^(8p + 7 - k - (h ? 0 : 4)).  Outputs: byte tables of H, H^2, H^4 (GCM
+// lane groups) and H^64 (wide), nibble tables of H^1..H^4 and of H^(2^b), b = 0..6 (wide).
+struct TablesArgs {
+  const u32x4* chains;  // 8 x 128 (ks_chain_exp order)
+  u32x4* htab;          // 3 x 4096: H, H^2, H^4
+  u32x4* h64;           // 4096
+  u32x4* ntab;          // 4 x 512: H^1..H^4
+  u32x4* wnib;          // 7 x 512: H^(2^b)
+};
+constexpr uint32_t kTabEntries = 4u * 4096u + 11u * 512u;
+
+__global__ __launch_bounds__(256) void gcm_tables_kernel(TablesArgs a) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kTabEntries) return;
+  // byte tables: 0..3 -> chain 0 (H), 1 (H^2), 3 (H^4), 7 (H^64)
+  if (e < 4u * 4096u) {
+    const uint32_t t = e >> 12, v = (e >> 4) & 255u, p = e & 15u;
+    const uint32_t ch = t == 0 ? 0u : t == 1 ? 1u : t == 2 ? 3u : 7u;
+    const u32x4* c = a.chains + ch * 128u + 8u * p + 7u;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (v & (1u << k)) acc ^= *(c - k);
+    if (t < 3u) a.htab[e] = acc;
+    else a.h64[e - 3u * 4096u] = acc;
+    return;
   }
+  // nibble tables: 0..3 -> H^1..H^4 (chains 0..3); 4..10 -> H^(2^b) (chains 0, 1, 3, 4, 5, 6, 7)
+  const uint32_t f = e - 4u * 4096u;
+  const uint32_t t = f >> 9, row = (f >> 4) & 31u, v = f & 15u, p = row >> 1, sh = (row & 1u) ? 0u : 4u;
+  const uint32_t b = t - 4u;
+  const uint32_t ch = t < 4u ? t : (b == 0u ? 0u : b == 1u ? 1u : b + 1u);
+  const u32x4* c = a.chains + ch * 128u + 8u * p + 7u - sh;
+  u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (v & (1u << k)) acc ^= *(c - k);
+  if (t < 4u) a.ntab[f] = acc;
+  else a.wnib[f - 4u * 512u] = acc;
 }
 
 }  // namespace dev

@@ -339,6 +339,33 @@ def test_derived_subkey_device_keyed(n, nrec, plan):
         aead.force_plan(0, 0)
 
 
+@pytest.mark.parametrize("n,nrec,wide,plan", [(100000, 3, (1, 2), None), (1 << 20, 2, (1, 0), None),
+                                           (65536, 9, (-1, 0), (4, 40)), (4097, 5, (-1, 0), (2, 3))])
+def test_derived_subkey_wide_and_pow2_segments(n, nrec, wide, plan):
+    """Device-keyed contexts on the wide plan (H^64 byte table and H^(2^b) nibble tables built
+    by the table kernel) and on multi-segment lane groups (G rounded to a power of two, combine
+    weights as products of H^(2^i)): bit-exact vs the oracle under K' = AES_K(V), forgery."""
+    base = aead.CipherCtx(KEY, "aes-128-ecb")
+    v = splitmix64_bytes(0x61200 + n, 16).tobytes()
+    kprime = oracle.ecb_encrypt(KEY, v)
+    pt = records(17 + n, nrec, n)
+    nonces = np.stack([np.frombuffer(oracle.nonce602(b"0", 3 + i), np.uint8) for i in range(nrec)])
+    aead.force_wide(*wide)
+    if plan:
+        aead.force_plan(*plan)
+    sub = aead.AeadCtx.derive_subkey(base, v)
+    L, nseg, G, r0 = aead.gcm_plan(sub, n, nrec)
+    assert (L == 64) == (wide[0] == 1) and (nseg == 1 or G & (G - 1) == 0), (L, nseg, G)
+    want = oracle.gcm_seal_batch(kprime, nonces, pt)
+    assert np.array_equal(gpu_seal(sub, nonces, pt), want), (L, nseg, G, r0)
+    forged = want.copy()
+    forged[nrec // 2, -3] ^= 1
+    back, st = gpu_open(sub, nonces, forged)
+    bad = nrec // 2
+    assert st[bad] == 0 and not back[bad].any()
+    assert all(st[i] == 1 and np.array_equal(back[i], pt[i]) for i in range(nrec) if i != bad)
+
+
 def test_rekey_subkey_reuses_context():
     """One context re-keyed per message (what a 602 sender thread does per MPI_Send)."""
     base = aead.AeadCtx(KEY)  # any context holding K serves as the base
