@@ -302,6 +302,64 @@ __device__ __forceinline__ u32x4 gmul_nib(u32x4 x, uint32_t tb) {
   return r;
 }
 
+// GCM-order field element as (hi, lo) big-endian halves of its 16 memory bytes.
+__device__ __forceinline__ void gf_split(u32x4 x, uint64_t& h, uint64_t& l) {
+  h = ((uint64_t)__builtin_bswap32(x[0]) << 32) | __builtin_bswap32(x[1]);
+  l = ((uint64_t)__builtin_bswap32(x[2]) << 32) | __builtin_bswap32(x[3]);
+}
+__device__ __forceinline__ u32x4 gf_join(uint64_t h, uint64_t l) {
+  return u32x4{__builtin_bswap32((uint32_t)(h >> 32)), __builtin_bswap32((uint32_t)h),
+               __builtin_bswap32((uint32_t)(l >> 32)), __builtin_bswap32((uint32_t)l)};
+}
+
+// X · x^s (0 <= s < 128) on (hi, lo) halves: the 128-bit right shift by s, whose shifted-out
+// coefficients (x^128 ..) fold back through x^128 = 1 + x + x^2 + x^7 — twice, the second fold
+// for the at most 7 bits the first one pushes past x^127.  Straight-line (no bit-serial loop).
+__device__ __forceinline__ void gf_mulx_pow(uint64_t& h, uint64_t& l, uint32_t s) {
+  uint64_t w0 = h, w1 = l, w2 = 0, w3 = 0;
+  if (s & 64u) {
+    w2 = w1;
+    w1 = w0;
+    w0 = 0;
+  }
+  const uint32_t q = s & 63u;
+  if (q) {
+    w3 = w2 << (64u - q);
+    w2 = (w2 >> q) | (w1 << (64u - q));
+    w1 = (w1 >> q) | (w0 << (64u - q));
+    w0 >>= q;
+  }
+  const uint64_t sp = (w3 << 63) ^ (w3 << 62) ^ (w3 << 57);
+  h = w0 ^ w2 ^ (w2 >> 1) ^ (w2 >> 2) ^ (w2 >> 7);
+  l = w1 ^ w3 ^ ((w3 >> 1) | (w2 << 63)) ^ ((w3 >> 2) | (w2 << 62)) ^ ((w3 >> 7) | (w2 << 57));
+  h ^= sp ^ (sp >> 1) ^ (sp >> 2) ^ (sp >> 7);
+}
+
+// Nibble-table row `row` (0..31) of P, built in LDS at tb + row*256 (the layout gmul_nib reads,
+// gf128_host.hpp build_nibble_table): entry v = XOR over set bits k of v of P · x^(c - k),
+// c = 8(row/2) + (row odd ? 7 : 3).  One variable shift, then three single shifts.
+__device__ __forceinline__ void nib_row_to_lds(u32x4 P, uint32_t row, uint32_t tb) {
+  uint64_t h, l;
+  gf_split(P, h, l);
+  gf_mulx_pow(h, l, 8u * (row >> 1) + ((row & 1u) ? 4u : 0u));  // P · x^(c - 3)
+  u32x4 u[4];
+#pragma unroll
+  for (int k = 3; k >= 0; --k) {
+    u[k] = gf_join(h, l);
+    const uint64_t lsb = 0 - (l & 1u);
+    l = (l >> 1) | (h << 63);
+    h = (h >> 1) ^ (0xE100000000000000ULL & lsb);
+  }
+#pragma unroll
+  for (uint32_t v = 0; v < 16u; ++v) {
+    u32x4 e = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (v & (1u << k)) e ^= u[k];
+    lds_st128(tb + row * 256u + v * 16u, e);
+  }
+}
+
 // Generic X · Y (both arbitrary, memory-order words), bit-serial SP 800-38D Algorithm 1.
 // Used only outside the hot loop (segment combination).
 __device__ __forceinline__ u32x4 gmul_generic(u32x4 x, u32x4 y) {

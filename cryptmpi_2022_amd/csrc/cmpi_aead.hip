@@ -13,6 +13,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <array>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -125,12 +126,9 @@ struct cmpi_ctx {
   cmpi::dev::RoundKeys drk{};
   Blk H{};
   DevTables* dt = nullptr;  // device
-  // per-G segment power tables, H^{kG}
+  // per-G combine multipliers H^{G·2^j}, j < 7 (host-keyed contexts; passed by value)
   mutable std::mutex mu;
-  mutable std::map<uint32_t, std::pair<u32x4*, uint32_t>> pw;
-  // wide decomposition (lazy): byte table of H^64, nibble tables of H^(2^b), b = 0..6
-  mutable u32x4* h64tab = nullptr;
-  mutable u32x4* wnib = nullptr;
+  mutable std::map<uint32_t, std::array<Blk, 7>> mj;
   // internal scratch (partials, status) and staging for *_host
   mutable void* scratch = nullptr;
   mutable size_t scratch_cap = 0;
@@ -248,68 +246,49 @@ size_t gcm_ws_bytes(const cmpi_ctx* c, const GcmPlan& p, size_t nrec) {
 
 // Byte table of H^64 (the wide kernel's Horner multiplier), built once per context.
 int get_h64tab(const cmpi_ctx* c, const u32x4** out) {
-  if (c->dev_keys) {  // built on the device by gcm_tables_kernel
-    *out = reinterpret_cast<const u32x4*>(c->dt->h64);
-    return CMPI_OK;
-  }
-  std::lock_guard<std::mutex> lk(c->mu);
-  if (!c->h64tab) {
-    std::vector<Blk> tab(4096);
-    cmpi::build_byte_table(cmpi::gf_pow(c->H, 64), tab.data());
-    u32x4* d = nullptr;
-    HIP_TRY(hipMalloc(&d, 4096 * 16));
-    HIP_TRY(hipMemcpy(d, tab.data(), 4096 * 16, hipMemcpyHostToDevice));
-    c->h64tab = d;
-  }
-  *out = c->h64tab;
+  *out = reinterpret_cast<const u32x4*>(c->dt->h64);  // ctx_new (host key) / gcm_tables_kernel
   return CMPI_OK;
 }
 
-// Lane weights of the wide kernel: nibble tables of H^(2^b), b = 0..6 (7 x 8 KiB), once per ctx.
+// Lane weights of the wide kernel: nibble tables of H^(2^b), b = 0..6 (7 x 8 KiB).
 int get_wnib(const cmpi_ctx* c, const u32x4** out) {
-  if (c->dev_keys) {
-    *out = reinterpret_cast<const u32x4*>(c->dt->wnib[0]);
-    return CMPI_OK;
-  }
-  std::lock_guard<std::mutex> lk(c->mu);
-  if (!c->wnib) {
-    std::vector<Blk> tab(7 * 512);
-    Blk p = c->H;
-    for (int b = 0; b < 7; ++b) {
-      cmpi::build_nibble_table(p, tab.data() + (size_t)b * 512);
-      p = cmpi::gf_mul(p, p);
-    }
-    u32x4* d = nullptr;
-    HIP_TRY(hipMalloc(&d, tab.size() * 16));
-    HIP_TRY(hipMemcpy(d, tab.data(), tab.size() * 16, hipMemcpyHostToDevice));
-    c->wnib = d;
-  }
-  *out = c->wnib;
+  *out = reinterpret_cast<const u32x4*>(c->dt->wnib[0]);
   return CMPI_OK;
 }
 
-int get_pw(const cmpi_ctx* c, uint32_t G, uint32_t nseg, const u32x4** out) {
-  std::lock_guard<std::mutex> lk(c->mu);
-  auto it = c->pw.find(G);
-  if (it != c->pw.end() && it->second.second >= nseg) {
-    *out = it->second.first;
+// Combine multipliers M_j = H^{G·2^j}, j < 7 (gcm_combine_kernel).  Host-keyed contexts: computed
+// here once per segment length G and passed in the kernel arguments (no allocation or copy on
+// the launch path, which also runs inside the multi-stream host pipeline); device-keyed:
+// H^(2^(log2 G + j)) in the context's device tables (written by the key-setup kernel).
+int get_mj(const cmpi_ctx* c, uint32_t G, cmpi::dev::GcmCombineArgs& ca) {
+  if (c->dev_keys) {
+    if (G & (G - 1u) || __builtin_ctz(G) + 7 > 32) return fail(CMPI_EINVAL, "device-keyed segment length");
+    ca.mjp = reinterpret_cast<const u32x4*>(c->dt->h2pow[__builtin_ctz(G)]);
     return CMPI_OK;
   }
-  uint32_t n = std::max<uint32_t>(nseg, it != c->pw.end() ? it->second.second * 2 : 64);
-  std::vector<Blk> h(n);
-  const Blk HG = cmpi::gf_pow(c->H, G);
-  h[0] = cmpi::gf_one();
-  for (uint32_t k = 1; k < n; ++k) h[k] = cmpi::gf_mul(h[k - 1], HG);
-  u32x4* d = nullptr;
-  HIP_TRY(hipMalloc(&d, (size_t)n * 16));
-  HIP_TRY(hipMemcpy(d, h.data(), (size_t)n * 16, hipMemcpyHostToDevice));
-  if (it != c->pw.end()) {
-    (void)hipFree(it->second.first);
-    it->second = {d, n};
-  } else {
-    c->pw[G] = {d, n};
+  std::lock_guard<std::mutex> lk(c->mu);
+  auto it = c->mj.find(G);
+  if (it == c->mj.end()) {
+    std::array<Blk, 7> m;
+    m[0] = cmpi::gf_pow(c->H, G);
+    for (int j = 1; j < 7; ++j) m[j] = cmpi::gf_mul(m[j - 1], m[j - 1]);
+    it = c->mj.emplace(G, m).first;
   }
-  *out = d;
+  ca.mjp = nullptr;
+  static_assert(sizeof(Blk) == sizeof(u32x4), "field element layout");
+  memcpy(ca.mjv, it->second.data(), sizeof(ca.mjv));
+  return CMPI_OK;
+}
+
+template <bool DEC>
+int launch_gcm_combine(const cmpi_ctx* c, cmpi::dev::GcmCombineArgs& ca, uint32_t G, hipStream_t st) {
+  int rc = get_mj(c, G, ca);
+  if (rc) return rc;
+  const uint32_t wpb = cmpi::dev::kCombineThreads / 64u;
+  const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((ca.nrec + wpb - 1u) / wpb, 2u * (uint32_t)c->ncu));
+  hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3(grid), dim3(cmpi::dev::kCombineThreads),
+                     cmpi::dev::kCombineLds, st, ca);
+  HIP_TRY(hipGetLastError());
   return CMPI_OK;
 }
 
@@ -390,7 +369,6 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.nflag = ns.flag;
   memcpy(a.nfix, ns.fix, sizeof a.nfix);
   a.sched = (uint32_t)g_sched.load();
-  const u32x4* pw = nullptr;
   if (p.wide) {
     if ((uint64_t)nrec * p.nseg * 16 > 0xFFFFFFFFull) return fail(CMPI_EINVAL, "too many chunks");
     uint8_t* ws = (uint8_t*)workspace;
@@ -404,10 +382,8 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
     a.S = p.S;
     a.nch = p.nseg;
-    const u32x4* pw = nullptr;
     int rc = get_h64tab(c, &a.htab);
     if (!rc) rc = get_wnib(c, &a.wtab);
-    if (!rc && !c->dev_keys) rc = get_pw(c, p.G, p.nseg, &pw);
     if (rc) return rc;
     auto fn = cmpi::dev::gcm_wide_kernel<DEC>;
     const size_t lds = 2 * 65536;
@@ -428,13 +404,8 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     ca.nseg = p.nseg;
     ca.partial = a.partial;
     ca.ekj0 = a.ekj0;
-    ca.pw = pw;  // chunk i weighted by H^{(nch-1-i)·64S}, as segments
-    ca.h2pow = reinterpret_cast<const u32x4*>(c->dt->h2pow[0]);
-    ca.glog = (uint32_t)__builtin_ctz(p.G);  // dev_keys: G = 64S is a power of two
     ca.status = status;
-    hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(cmpi::dev::kCombineThreads), 0, st, ca);
-    HIP_TRY(hipGetLastError());
-    return CMPI_OK;
+    return launch_gcm_combine<DEC>(c, ca, p.G, st);  // chunk i weighted by H^{(nch-1-i)·64S}, as segments
   }
   if (p.nseg > 1) {
     uint8_t* ws = (uint8_t*)workspace;
@@ -446,10 +417,6 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
     a.partial = reinterpret_cast<u32x4*>(ws);
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
-    if (!c->dev_keys) {  // device-keyed: weights from H^(2^i) in the combine (G = 2^g)
-      int rc = get_pw(c, p.G, p.nseg, &pw);
-      if (rc) return rc;
-    }
   }
   const size_t lds = cmpi::dev::gcm_lds_bytes(p.L);
   const uint64_t want = ((uint64_t)a.ngroups * p.L + kGcmThreads - 1) / kGcmThreads;
@@ -473,12 +440,9 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     ca.nseg = p.nseg;
     ca.partial = a.partial;
     ca.ekj0 = a.ekj0;
-    ca.pw = pw;
-    ca.h2pow = reinterpret_cast<const u32x4*>(c->dt->h2pow[0]);
-    ca.glog = (uint32_t)__builtin_ctz(p.G);
     ca.status = status;
-    hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3((uint32_t)nrec), dim3(cmpi::dev::kCombineThreads), 0, st, ca);
-    HIP_TRY(hipGetLastError());
+    rc = launch_gcm_combine<DEC>(c, ca, p.G, st);
+    if (rc) return rc;
   }
   return CMPI_OK;
 }
@@ -923,6 +887,13 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
     cmpi::build_byte_table(H4, reinterpret_cast<Blk*>(ht->htab[2]));
     const Blk pw[4] = {c->H, H2, H3, H4};
     for (int i = 0; i < 4; ++i) cmpi::build_nibble_table(pw[i], reinterpret_cast<Blk*>(ht->ntab[i]));
+    // wide plan: byte table of H^64, nibble tables of H^(2^b), b < 7
+    Blk p = c->H;
+    for (int b = 0; b < 7; ++b) {
+      cmpi::build_nibble_table(p, reinterpret_cast<Blk*>(ht->wnib[b]));
+      if (b == 6) cmpi::build_byte_table(p, reinterpret_cast<Blk*>(ht->h64));  // p = H^64
+      p = cmpi::gf_mul(p, p);
+    }
   }
   if (alg == CMPI_AES_128_OCB) {
     // RFC 7253 §4.1: L_* = E_K(0), L_$ = double(L_*), L_0 = double(L_$), L_i = double(L_{i-1})
@@ -958,9 +929,6 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   // calls, the key-setup kernel of a derived sub-key): drain the device before its tables,
   // scratch and staging go back to the allocator.
   (void)hipDeviceSynchronize();
-  for (auto& kv : c->pw) (void)hipFree(kv.second.first);
-  if (c->wnib) (void)hipFree(c->wnib);
-  if (c->h64tab) (void)hipFree(c->h64tab);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
@@ -1215,11 +1183,7 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   if (rc) return rc;
   {
     std::lock_guard<std::mutex> lk(dst->mu);
-    for (auto& kv : dst->pw) (void)hipFree(kv.second.first);
-    dst->pw.clear();
-    if (dst->h64tab) (void)hipFree(dst->h64tab);
-    if (dst->wnib) (void)hipFree(dst->wnib);
-    dst->h64tab = dst->wnib = nullptr;
+    dst->mj.clear();
     dst->dev_keys = true;
     memset(dst->key, 0, 16);
     memset(&dst->rk, 0, sizeof dst->rk);

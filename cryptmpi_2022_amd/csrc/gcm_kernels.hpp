@@ -413,63 +413,71 @@ struct GcmCombineArgs {
   uint32_t len, nb, nrec, nseg;
   const u32x4* partial;  // nrec*nseg
   const u32x4* ekj0;     // nrec
-  const u32x4* pw;       // pw[k] = H^{k*G}, k < nseg (host-keyed contexts), or null and:
-  const u32x4* h2pow;    // H^(2^i), i < 32, with G = 2^glog (device-keyed contexts)
-  uint32_t glog;
   int32_t* status;
+  const u32x4* mjp;      // device-keyed: M_j = H^{G·2^j} = H^(2^(log2 G + j)) in HBM, j < 7; or null:
+  u32x4 mjv[7];          // host-keyed: M_j by value
 };
 
-// One 256-thread block per record: Y = XOR_s partial[s] · H^{(nseg-1-s)·G}; tag = Y ^ E_K(J0).
-// One generic multiply per thread for up to 256 partials (the multiplies' latency, not their
-// count, is what a record waits for).
+// One wave per record: Y = XOR_s partial[s] · H^{(nseg-1-s)·G}; tag = Y ^ E_K(J0).
+// With k = nseg-1-s = lane + 64m, lane `lane` folds its partials by Horner in M_6 = H^{64G}
+// (m descending; a lane with fewer partials folds zeros) and multiplies the result by
+// M^lane = product of M_j over the set bits j of lane: at most ceil(nseg/64) - 1 + 6
+// multiplies in sequence, each by an LDS nibble table of one M_j (gmul_nib) — the block builds
+// those tables once (one row per thread, nib_row_to_lds) for every record it handles.
+// (Replaced a bit-serial 128-step generic multiply per partial: ~4 us each in sequence.)
 constexpr uint32_t kCombineThreads = 256u;
+constexpr size_t kCombineLds = 7u * 8192u;
 template <bool DECRYPT>
 __global__ __launch_bounds__(256) void gcm_combine_kernel(GcmCombineArgs a) {
-  __shared__ u32x4 red[kCombineThreads / 64u];
-  const uint32_t r = blockIdx.x;
+  const uint32_t nseg = a.nseg;
+  const uint32_t nt = nseg > 64u ? 7u : nseg > 1u ? 32u - __builtin_clz(nseg - 1u) : 0u;
   const uint32_t t = threadIdx.x, lane = t & 63u;
-  u32x4 y = {0u, 0u, 0u, 0u};
-  for (uint32_t s = t; s < a.nseg; s += blockDim.x) {
-    const u32x4 p = a.partial[(uint64_t)r * a.nseg + s];
-    const uint32_t k = a.nseg - 1u - s;
-    if (a.pw) {
-      y ^= k == 0u ? p : gmul_generic32(p, a.pw[k]);
-    } else {  // H^{k·2^glog} = product of H^(2^(glog + j)) over the set bits j of k
-      u32x4 q = p;
-      for (uint32_t m = k, j = a.glog; m; m >>= 1, ++j)
-        if (m & 1u) q = gmul_generic32(q, a.h2pow[j]);
-      y ^= q;
-    }
-  }
+  if (t < nt * 32u) {
+    const uint32_t j = t >> 5;
+    u32x4 P = a.mjv[0];
 #pragma unroll
-  for (int m = 1; m < 64; m <<= 1) y ^= shfl_xor4(y, m);
-  if (lane == 0u) red[t >> 6] = y;
+    for (uint32_t q = 1; q < 7u; ++q)
+      if (q == j) P = a.mjv[q];
+    if (a.mjp) P = a.mjp[j];
+    nib_row_to_lds(P, t & 31u, j * 8192u);
+  }
   __syncthreads();
-  if (t >= 64u) return;
-  y = red[0];
-  for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) y ^= red[w];
-  if (a.ekj0) y ^= a.ekj0[r];  // null: E_K(J0) already inside the partials
-  int ok = 1;
-  if (!DECRYPT) {
-    if (lane == 0) {
-      uint8_t* tp = a.out + (uint64_t)r * a.out_stride + a.len;
-      st_blk(tp, y);
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t mmax = (nseg + 63u) >> 6;  // Horner steps (wave-uniform)
+  for (uint32_t r = blockIdx.x * wpb + (t >> 6); r < a.nrec; r += gridDim.x * wpb) {
+    const u32x4* part = a.partial + (uint64_t)r * nseg;
+    u32x4 y = {0u, 0u, 0u, 0u};
+    for (uint32_t m = mmax; m-- > 0u;) {
+      if (m + 1u < mmax) y = gmul_nib(y, 6u * 8192u);
+      const uint32_t k = lane + 64u * m;
+      if (k < nseg) y ^= part[nseg - 1u - k];
     }
-    return;
-  }
-  if (lane == 0) {
-    const uint8_t* tp = a.in + (uint64_t)r * a.in_stride + a.len;
-    const u32x4 tg = ld_blk(tp);
-    const u32x4 d = tg ^ y;
-    ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
-    if (a.status) a.status[r] = ok;
-  }
-  ok = __shfl(ok, 0);
-  if (!ok) {
-    uint8_t* o = a.out + (uint64_t)r * a.out_stride;
-    const uint32_t full = a.len & ~3u;
-    for (uint32_t i = lane * 4u; i < full; i += 64u * 4u) *reinterpret_cast<u32a*>(o + i) = 0u;
-    for (uint32_t i = full + lane; i < a.len; i += 64u) o[i] = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 6u; ++j) {
+      if ((1u << j) >= nseg) break;  // wave-uniform: lane < nseg needs only bits j < nt
+      const u32x4 q = gmul_nib(y, j * 8192u);
+      if ((lane >> j) & 1u) y = q;
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) y ^= shfl_xor4(y, m);
+    if (a.ekj0) y ^= a.ekj0[r];  // null: E_K(J0) already inside the partials
+    if (!DECRYPT) {
+      if (lane == 0u) st_blk(a.out + (uint64_t)r * a.out_stride + a.len, y);
+      continue;
+    }
+    int ok = 1;
+    if (lane == 0u) {
+      const u32x4 d = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len) ^ y;
+      ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+      if (a.status) a.status[r] = ok;
+    }
+    ok = __shfl(ok, 0);
+    if (!ok) {
+      uint8_t* o = a.out + (uint64_t)r * a.out_stride;
+      const uint32_t full = a.len & ~3u;
+      for (uint32_t i = lane * 4u; i < full; i += 64u * 4u) *reinterpret_cast<u32a*>(o + i) = 0u;
+      for (uint32_t i = full + lane; i < a.len; i += 64u) o[i] = 0u;
+    }
   }
 }
 

@@ -24,16 +24,6 @@ struct KeysetupArgs {
   u32x4* chains;        // out: basis chains P·x^i (i < 128) of P = H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
 };
 
-// GCM-order field element as (hi, lo) big-endian halves of its 16 memory bytes.
-__device__ __forceinline__ void gf_split(u32x4 x, uint64_t& h, uint64_t& l) {
-  h = ((uint64_t)__builtin_bswap32(x[0]) << 32) | __builtin_bswap32(x[1]);
-  l = ((uint64_t)__builtin_bswap32(x[2]) << 32) | __builtin_bswap32(x[3]);
-}
-__device__ __forceinline__ u32x4 gf_join(uint64_t h, uint64_t l) {
-  return u32x4{__builtin_bswap32((uint32_t)(h >> 32)), __builtin_bswap32((uint32_t)h),
-               __builtin_bswap32((uint32_t)(l >> 32)), __builtin_bswap32((uint32_t)l)};
-}
-
 // The 8 chained multipliers: index -> exponent of H.
 __host__ __device__ constexpr uint32_t ks_chain_exp(uint32_t j) {
   return j == 0 ? 1u : j == 1 ? 2u : j == 2 ? 3u : j == 3 ? 4u : j == 4 ? 8u : j == 5 ? 16u : j == 6 ? 32u : 64u;

@@ -32,7 +32,9 @@ def med(fn, reps=9):
     return sorted(ts)[len(ts) // 2]
 
 
-for n in (1 << 16, 1 << 20, 8 << 20):
+steps = [int(x) for x in os.environ.get("AB602_STEPS", "0").split(",")]
+for n, S in [(n, S) for n in (1 << 16, 1 << 20, 8 << 20) for S in steps]:
+    aead.force_wide(1 if S else 0, S)
     plan = frame.plan602(n, series_threads=8)
     rand16 = bytes(range(100, 116))
     hdr = frame.header602(plan, rand16)
@@ -59,9 +61,11 @@ for n in (1 << 16, 1 << 20, 8 << 20):
     torch.cuda.synchronize()
     ok = bool((st == 1).all()) and torch.equal(back, pt)
     t_rk, t_seal, t_both, t_open = med(rekey), med(seal), med(both), med(opn)
-    res[f"602_{n >> 10}KiB"] = {"plan": plan.as_dict(), "rekey_us": round(t_rk * 1e3, 1),
+    key = f"602_{n >> 10}KiB" + (f"_S{S}" if S else "")
+    res[key] = {"plan": plan.as_dict(), "gcm_plan": aead.gcm_plan(seg, plan.chop, plan.nseg), "rekey_us": round(t_rk * 1e3, 1),
                                 "seal_us": round(t_seal * 1e3, 1), "rekey_seal_us": round(t_both * 1e3, 1),
                                 "open_us": round(t_open * 1e3, 1),
                                 "seal_GiBps": round(n / (t_both * 1e-3) / 2**30, 1), "round_trip_ok": ok}
-    print(f"602_{n >> 10}KiB", res[f"602_{n >> 10}KiB"], flush=True)
+    print(key, {k: v for k, v in res[key].items() if k != "plan"}, flush=True)
+aead.force_wide(0, 0)
 print(json.dumps(res))
