@@ -227,9 +227,19 @@ __device__ __forceinline__ void aes128_dec(const RoundKeys& k, const RowLanes& L
 // ---------------------------------------------------------------- table staging
 // Row image from a 256-word T0 (Te0 or Td0): row x = [T0[x] x32 | rotl8(T0[x]) x32].
 __device__ __forceinline__ void stage_rows(const uint32_t* __restrict__ t0, uint32_t base) {
-  for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) {
-    const uint32_t v = t0[i >> 6];
-    lds_st32(base + i * 4u, (i & 32u) ? rotl8(v) : v);
+  // entry e fills 64 words at base + 256e: 32 copies of Te0[e], then 32 of rotl8 (Te1[e]).
+  // Four threads per entry, one global load and four 16-byte LDS stores each (one pass at
+  // 1024 threads; a word-per-iteration loop paid the global-load latency 16 times).
+  for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) {
+    const uint32_t e = i >> 2, s = i & 3u;
+    uint32_t v = t0[e];
+    if (s >= 2u) v = rotl8(v);
+    const u32x4 q = {v, v, v, v};
+    const uint32_t o = base + e * 256u + s * 64u;
+    lds_st128(o, q);
+    lds_st128(o + 16u, q);
+    lds_st128(o + 32u, q);
+    lds_st128(o + 48u, q);
   }
 }
 // 32-way replicated 256-word table with 128-B rows (the inverse S-box image).
@@ -237,7 +247,16 @@ __device__ __forceinline__ void stage_rep32(const uint32_t* __restrict__ t, uint
   for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x) lds_st32(base + i * 4u, t[i >> 5]);
 }
 __device__ __forceinline__ void stage_copy(const u32x4* __restrict__ src, uint32_t dst_off, uint32_t n16) {
-  for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) lds_st128(dst_off + i * 16u, src[i]);
+  const uint32_t step = blockDim.x;
+  uint32_t i = threadIdx.x;
+  for (; i + 3u * step < n16; i += 4u * step) {  // four loads in flight per thread
+    const u32x4 a0 = src[i], a1 = src[i + step], a2 = src[i + 2u * step], a3 = src[i + 3u * step];
+    lds_st128(dst_off + i * 16u, a0);
+    lds_st128(dst_off + (i + step) * 16u, a1);
+    lds_st128(dst_off + (i + 2u * step) * 16u, a2);
+    lds_st128(dst_off + (i + 3u * step) * 16u, a3);
+  }
+  for (; i < n16; i += step) lds_st128(dst_off + i * 16u, src[i]);
 }
 
 // ---------------------------------------------------------------- GHASH
@@ -286,18 +305,28 @@ __device__ __forceinline__ u32x4 gmul_byte(u32x4 x, const GhashLane& g) {
 }
 
 // X · P with an 8 KiB nibble table of P at LDS byte offset `tb` (multiple of 8 KiB).
+// The 32 lookups go out in batches of 8 (one s_waitcnt per batch): written as one loop the
+// compiler, short of registers in the wide kernel, paired them with a wait after every two
+// reads — 16 LDS round trips (~1 us) per multiply.
 __device__ __forceinline__ u32x4 gmul_nib(u32x4 x, uint32_t tb) {
   u32x4 r = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int p = 0; p < 16; ++p) {
-    const uint32_t w = x[p >> 2];
-    const int sh = 8 * (p & 3);
-    const uint32_t hi = (w >> sh) & 0xf0u;                              // (v >> 4) * 16
-    const uint32_t lo = (sh == 0 ? (w << 4) : (w >> (sh - 4))) & 0xf0u;  // (v & 15) * 16
-    const u32x4 e1 = lds128((hi | tb) + (uint32_t)p * 512u);
-    const u32x4 e2 = lds128((lo | tb) + (uint32_t)p * 512u + 256u);
+  for (int q = 0; q < 16; q += 4) {
+    u32x4 e[8];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) r[c] = xor3(r[c], e1[c], e2[c]);
+    for (int t = 0; t < 4; ++t) {
+      const int p = q + t;
+      const uint32_t w = x[p >> 2];
+      const int sh = 8 * (p & 3);
+      const uint32_t hi = (w >> sh) & 0xf0u;                              // (v >> 4) * 16
+      const uint32_t lo = (sh == 0 ? (w << 4) : (w >> (sh - 4))) & 0xf0u;  // (v & 15) * 16
+      e[2 * t] = lds128((hi | tb) + (uint32_t)p * 512u);
+      e[2 * t + 1] = lds128((lo | tb) + (uint32_t)p * 512u + 256u);
+    }
+#pragma unroll
+    for (int t = 0; t < 8; t += 2)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) r[c] = xor3(r[c], e[t][c], e[t + 1][c]);
   }
   return r;
 }
@@ -424,6 +453,15 @@ __device__ __forceinline__ void rotate_prio(uint32_t t) {
     case 2: __builtin_amdgcn_s_setprio(2); break;
     default: __builtin_amdgcn_s_setprio(3); break;
   }
+}
+
+__device__ __forceinline__ u32x4 shfl_down4(u32x4 v, uint32_t d) {
+  u32x4 r;
+  r[0] = __shfl_down((int)v[0], d);
+  r[1] = __shfl_down((int)v[1], d);
+  r[2] = __shfl_down((int)v[2], d);
+  r[3] = __shfl_down((int)v[3], d);
+  return r;
 }
 
 __device__ __forceinline__ u32x4 shfl_xor4(u32x4 v, int m) {

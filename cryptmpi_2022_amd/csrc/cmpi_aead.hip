@@ -174,6 +174,8 @@ int set_lds_attr(const void* fn, int device, size_t lds) {
 }
 
 // ---------------------------------------------------------------- GCM launch planning
+// wide plan: a wave's fixed cost (table staging, lane weights) in units of one 64-block step
+constexpr uint64_t kWideFixedSteps = 4;
 struct GcmPlan {
   int L;
   uint32_t nb, nseg, G, r0;
@@ -188,6 +190,7 @@ std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
 std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
+std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics: wide-kernel phase timestamps
 std::atomic<int> g_sched{7};         // wave-priority rotation: bit 0 GCM, bit 1 CTR, bit 2 OCB
 std::atomic<int> g_gcm_ablation{0};  // timing ablation of the L=4 seal kernel (tools/ablate.py)  // LDS requested by the CTR kernel (occupancy experiments)
 
@@ -215,15 +218,29 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   const int fw = g_force_wide.load();
   const bool wide_ok = p.nb >= 64;
   if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target && nx >= 1024))) {
+    // A round = one wave per (record, chunk) on every CU (W waves); a wave's time ~ (fixed
+    // staging/weight phases) + S steps.  Chunks are cut from the end with chunk 0 absorbing the
+    // remainder (G <= its length < 2G), so 1 MiB records (nx = 2^16 + 1) split into exactly
+    // 2^16 / G chunks instead of one extra 1-block chunk that would start a second round.
+    const uint64_t W = (uint64_t)c->ncu * (kGcmThreads / 64);
+    const uint64_t smax = std::max<uint64_t>(1, nx / 64);
     uint64_t S = g_force_S.load();
-    if (!S) S = std::max<uint64_t>(4, (uint64_t)nrec * nx / (64ull * c->ncu * (kGcmThreads / 64)));
-    S = std::min<uint64_t>(S, (nx + 63) / 64);
+    if (!S) {
+      double best = 1e300;
+      for (uint64_t s = std::min<uint64_t>(2, smax); s <= smax; s = c->dev_keys ? 2 * s : s + 1) {
+        const uint64_t units = (uint64_t)nrec * std::max<uint64_t>(1, nx / (64 * s));
+        const double est = (double)((units + W - 1) / W) * (double)(kWideFixedSteps + s);
+        if (est < best) best = est, S = s;
+        if (units <= W / 2) break;  // one round already: longer chunks only lengthen it
+      }
+    }
+    S = std::min<uint64_t>(std::max<uint64_t>(S, 1), smax);
     if (c->dev_keys) S = (uint64_t)1 << (63 - __builtin_clzll(S));  // chunk weights from H^(2^i)
     p.wide = true;
     p.S = (uint32_t)S;
     p.L = 64;
     p.G = (uint32_t)(64 * S);
-    p.nseg = (uint32_t)((nx + p.G - 1) / p.G);
+    p.nseg = (uint32_t)std::max<uint64_t>(1, nx / p.G);
     p.r0 = (uint32_t)(nx - (uint64_t)(p.nseg - 1) * p.G);
     return p;
   }
@@ -385,6 +402,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     int rc = get_h64tab(c, &a.htab);
     if (!rc) rc = get_wnib(c, &a.wtab);
     if (rc) return rc;
+    a.probe = g_wide_probe.load();
     auto fn = cmpi::dev::gcm_wide_kernel<DEC>;
     const size_t lds = 2 * 65536;
     if ((rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds))) return rc;
@@ -977,6 +995,8 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
   g_force_L.store(lanes_per_record == 1 || lanes_per_record == 2 || lanes_per_record == 4 ? lanes_per_record : 0);
   g_force_nseg.store(segments);
 }
+
+void cmpi_debug_set_wide_probe(void* buf) { g_wide_probe.store(reinterpret_cast<uint64_t*>(buf)); }
 
 void cmpi_debug_set_gcm_prefetch(int slots) { g_gcm_pf.store(slots == 3 || slots == 4 || slots == 6 ? slots : 2); }
 

@@ -56,6 +56,7 @@ struct GcmArgs {
   // nibble tables of H^(2^b), b = 0..6 (lane weights)
   const u32x4* wtab;
   uint32_t S, nch;
+  uint64_t* probe;  // diagnostics (cmpi_debug_set_wide_probe): per-WG phase timestamps, or null
   RoundKeys rk;
 };
 
@@ -289,7 +290,8 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
 
 // ---------------------------------------------------------------- wide decomposition
 // Few long records (the naive Alltoall's p peer blocks of 1 MiB, alltoall.c:795-834): a record's
-// X-sequence is cut from the END into chunks of C = 64*S X-blocks (chunk 0 may be shorter) and
+// X-sequence is cut from the END into chunks of C = 64*S X-blocks (chunk 0 takes the remainder:
+// C <= its length < 2C, ceil(len/64) steps) and
 // every (record, chunk) is ONE wavefront.  At step k lane q owns X position base + 64k + q, so
 // each wave-instruction moves 1 KiB of contiguous record data, and the lane folds its blocks
 // into a Horner accumulator with multiplier H^64 (byte table of H^64 in LDS).  Lane q's last
@@ -303,6 +305,8 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
 // seven restaged conflict-free byte tables instead of the nibble tables were slower, 184.)
 template <bool DECRYPT>
 __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
+  const bool prb = a.probe && threadIdx.x == 0u;
+  if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
   stage_rows(a.te0, kGcmRows);
 
   const RoundKeys rk = load_round_keys(a.rk, a.rkp);  // folded (host / keysetup kernel)
@@ -327,11 +331,15 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
     __syncthreads();                // [0, 64K) is free: the previous round's weights are done
     stage_copy(a.htab, 0u, 4096u);  // byte table of H^64
     __syncthreads();
+    if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 1u] = wall_clock64();
     u32x4 acc = {0u, 0u, 0u, 0u};
     if (active) {
       const uint32_t r = u / a.nch;
       const uint32_t i = u - r * a.nch;
-      const int32_t base = nx - (int32_t)(a.nch - i) * C;  // position of step 0, lane 0 (may be < 0)
+      // chunk 0 runs ceil(r0/64) steps over [0, r0) (G <= r0 < 2G); chunk i > 0 runs S steps
+      const uint32_t steps = i == 0u ? (a.r0 + 63u) >> 6 : a.S;
+      const int32_t base = i == 0u ? (int32_t)a.r0 - 64 * (int32_t)steps  // step 0, lane 0 (may be < 0)
+                                   : nx - (int32_t)(a.nch - i) * C;
       const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
       uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
       uint32_t n0, n1, n2;
@@ -378,11 +386,11 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
       };
       u32x4 va = prefetch(0), vb = prefetch(1);
       uint32_t it = 0;
-      for (uint32_t k = 0; k < a.S; k += 2u) {
+      for (uint32_t k = 0; k < steps; k += 2u) {
         if (a.sched & 1u) rotate_prio(it++);
         consume(k, va);
         va = prefetch(k + 2u);
-        if (k + 1u < a.S) consume(k + 1u, vb);
+        if (k + 1u < steps) consume(k + 1u, vb);
         vb = prefetch(k + 3u);
       }
       if (i == 0u) {  // E_K(J0) for the combine kernel
@@ -390,10 +398,13 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
         if (lane == 0u) a.ekj0[r] = e;
       }
     }
+    if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 2u] = wall_clock64();
     __syncthreads();  // every wave is past its Horner loop: [0, 64K) takes the weight tables
+    if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 3u] = wall_clock64();
     stage_copy(a.wtab, 0u, 7u * 512u);  // nibble tables of H^(2^b), b = 0..6, 8 KiB apart
     __syncthreads();
-    if (active) {
+    if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 4u] = wall_clock64();
+    if (active && (a.sched & 8u)) {  // A/B: per-lane weights (previous scheme)
 #pragma unroll
       for (uint32_t b = 0; b < 7u; ++b) {
         const u32x4 m = gmul_nib(acc, b * 8192u);
@@ -402,7 +413,25 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
 #pragma unroll
       for (int m = 1; m < 64; m <<= 1) acc ^= shfl_xor4(acc, m);
       if (lane == 0u) a.partial[u] = acc;
+    } else if (active) {
+      // binary tree over the lanes: level b folds lane q + 2^b into lane q (q = 0 mod 2^(b+1))
+      // with weight H^(2^b), so lane 0 ends with XOR_q acc_q · H^(63-q); one more H gives
+      // H^(64-q).  Only the folding lanes multiply: 64 lane-multiplies per wave instead of 448.
+#pragma unroll
+      for (uint32_t b = 0; b < 6u; ++b) {
+        const u32x4 up = shfl_down4(acc, 1u << b);
+        if ((lane & ((2u << b) - 1u)) == 0u) {
+          asm volatile("" ::: "memory");  // keep the branch: only the folding lanes read LDS
+          acc = gmul_nib(acc, b * 8192u) ^ up;
+        }
+      }
+      if (lane == 0u) a.partial[u] = gmul_nib(acc, 0u);
     }
+    if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 5u] = wall_clock64();
+  }
+  if (a.probe) {
+    __syncthreads();
+    if (prb) a.probe[blockIdx.x * 8u + 6u] = wall_clock64();
   }
 }
 

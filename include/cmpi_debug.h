@@ -29,6 +29,10 @@ void cmpi_debug_set_sched(int mode);
 void cmpi_debug_set_host_chunk(size_t bytes);
 /* GCM lane-group kernel: input prefetch depth in slots (2, 3, 4 or 6; anything else = 2). */
 void cmpi_debug_set_gcm_prefetch(int slots);
+/* Diagnostics: when buf (device, >= 8 x grid u64) is non-null, every gcm_wide_kernel workgroup
+   writes wall-clock (100 MHz) timestamps of its phases at buf[8*block + 0..6]: start, tables
+   staged, own Horner done, all Horner done, weight tables staged, weights done, end. */
+void cmpi_debug_set_wide_probe(void* buf);
 /* Wide GCM decomposition (one wavefront per 64*steps-block chunk of a record, for few long
  * records): mode 0 automatic, 1 always when legal (host-keyed context, >= 64 data blocks),
  * -1 never; steps per chunk (0 = automatic). */

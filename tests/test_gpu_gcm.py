@@ -175,12 +175,15 @@ def test_large_records_multisegment():
 @pytest.mark.parametrize("n,nrec,steps", [(1024, 3, 1), (1040, 2, 1), (4097, 3, 2), (65535, 2, 4), (100000, 3, 3),
                                           (1 << 20, 2, 0), (64 * 16 * 5 - 16, 2, 5)])
 def test_wide_decomposition(n, nrec, steps):
-    """Wide plan (one wave per 64*steps-block chunk; chunk 0 ragged; lane-weighted partials):
-    bit-exact seal, round trip, forged record zero-filled, unaligned wire layout."""
+    """Wide plan (one wave per 64*steps-block chunk; chunk 0 takes the remainder, G <= r0 < 2G
+    or the whole record; lane-weighted partials): bit-exact seal, round trip, forged record
+    zero-filled, unaligned wire layout."""
     aead.force_wide(1, steps)
     ctx = aead.AeadCtx(KEY)
     L, nch, G, r0 = aead.gcm_plan(ctx, n, nrec)
-    assert L == 64 and G % 64 == 0 and 1 <= r0 <= G and nch == -(-(n // 16 + (n % 16 > 0) + 1) // G)
+    nx = n // 16 + (n % 16 > 0) + 1
+    assert L == 64 and G % 64 == 0 and nch == max(1, nx // G) and r0 == nx - (nch - 1) * G
+    assert r0 < 2 * G or nch == 1
     pt = records(0x3100 + n, nrec, n)
     nonces = random_nonces(0x3200 + n, nrec)
     want = oracle.gcm_seal_batch(KEY, nonces, pt)
