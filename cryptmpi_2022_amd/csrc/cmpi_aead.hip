@@ -83,21 +83,21 @@ struct DevTables {
   uint8_t ntab[kNibTables][kNibTab];
   uint8_t ltab[66][16];          // OCB: L_*, L_$, L_0..L_63
   // device-keyed (602 sub-key) contexts: written by gcm_keysetup_kernel / gcm_tables_kernel
-  uint8_t sqtab[kByteTab];       // squaring map byte table (key independent, from the host)
+  uint8_t sqmat[31][128][16];    // columns of X -> X^(2^i), i = 1..31 (key independent, host)
   uint8_t h2pow[32][16];         // H^(2^i)
   uint8_t chains[8][128][16];    // basis chains of H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
   uint8_t h64[kByteTab];         // byte table of H^64 (wide plan)
   uint8_t wnib[7][kNibTab];      // nibble tables of H^(2^b), b < 7 (wide plan)
 };
 
-// The squaring-map table, built once per process.
-const std::vector<Blk>& sq_table() {
-  static const std::vector<Blk> t = [] {
-    std::vector<Blk> v(4096);
-    cmpi::build_sq_table(v.data());
-    return v;
+// Columns of the squaring maps X -> X^(2^i) (key setup of device-derived keys), once per process.
+const std::vector<Blk>& sq_columns() {
+  static const std::vector<Blk> v = [] {
+    std::vector<Blk> m(31 * 128);
+    cmpi::build_sq_columns(m.data());
+    return m;
   }();
-  return t;
+  return v;
 }
 
 }  // namespace
@@ -890,7 +890,7 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
     memcpy(ht->keys, fk.w, sizeof fk.w);
   }
   memcpy(ht->keys + 48, c->H.b, 16);
-  memcpy(ht->sqtab, sq_table().data(), sizeof ht->sqtab);
+  memcpy(ht->sqmat, sq_columns().data(), sizeof ht->sqmat);
   {
     Blk p = c->H;
     for (int i = 0; i < 32; ++i) {
@@ -1189,7 +1189,7 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   memcpy(a.v, v, 16);
   a.mode = 1;
   a.te0 = dst->dt->te0;
-  a.sqtab = reinterpret_cast<const u32x4*>(dst->dt->sqtab);
+  a.sqmat = reinterpret_cast<const u32x4*>(dst->dt->sqmat[0]);
   a.keys = dst->dt->keys;
   a.h2pow = reinterpret_cast<u32x4*>(dst->dt->h2pow[0]);
   a.chains = reinterpret_cast<u32x4*>(dst->dt->chains[0]);

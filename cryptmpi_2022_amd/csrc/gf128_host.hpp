@@ -81,22 +81,15 @@ inline void build_byte_table(const Blk& P, Blk* tab) {
   }
 }
 
-// Byte table of the squaring map X -> X^2 (GF(2)-linear in characteristic 2), same [v][p]
-// layout as build_byte_table: tab[v*16 + p] = (block with byte p = v)^2.  Key independent.
-inline void build_sq_table(Blk* tab) {
-  for (int p = 0; p < 16; ++p) {
-    Blk basis[8];
-    for (int k = 0; k < 8; ++k) {
-      Blk e{};
-      e.b[p] = (uint8_t)(1u << k);
-      basis[k] = gf_mul(e, e);
-    }
-    for (int v = 0; v < 256; ++v) {
-      Blk acc{};
-      for (int k = 0; k < 8; ++k)
-        if (v & (1 << k))
-          for (int i = 0; i < 16; ++i) acc.b[i] ^= basis[k].b[i];
-      tab[v * 16 + p] = acc;
+// Columns of the linear maps X -> X^(2^i), i = 1..31: mat[(i-1)*128 + k] = (x^k)^(2^i), where
+// x^k is the element with only GCM-order bit k set (byte k/8, bit 7 - k%8).  31 x 2 KiB.
+inline void build_sq_columns(Blk* mat) {
+  for (int k = 0; k < 128; ++k) {
+    Blk v{};
+    v.b[k >> 3] = (uint8_t)(0x80u >> (k & 7));
+    for (int i = 1; i <= 31; ++i) {
+      v = gf_mul(v, v);
+      mat[(i - 1) * 128 + k] = v;
     }
   }
 }

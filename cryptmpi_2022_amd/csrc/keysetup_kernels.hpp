@@ -18,7 +18,8 @@ struct KeysetupArgs {
   uint32_t v[4];        // mode 0: K' itself; mode 1: V
   uint32_t mode;
   const uint32_t* te0;  // Te0 (global)
-  const u32x4* sqtab;   // byte table of the squaring map X -> X^2 (key independent)
+  const u32x4* sqmat;   // [i-1][k] = (x^k)^(2^i), i = 1..31, k < 128: columns of the linear maps
+                        // X -> X^(2^i) (key independent, host-built once per process)
   uint32_t* keys;       // out: [0..43] round keys of K' (folded), [48..51] H = E_K'(0)
   u32x4* h2pow;         // out: H^(2^i), i < 32
   u32x4* chains;        // out: basis chains P·x^i (i < 128) of P = H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
@@ -29,18 +30,23 @@ __host__ __device__ constexpr uint32_t ks_chain_exp(uint32_t j) {
   return j == 0 ? 1u : j == 1 ? 2u : j == 2 ? 3u : j == 3 ? 4u : j == 4 ? 8u : j == 5 ? 16u : j == 6 ? 32u : 64u;
 }
 
-// LDS (dynamic only: offsets are addresses): squaring byte table @0 (64 KiB, read by
-// gmul_byte), AES row image @64K (64 KiB), S-box bytes @128K (256 words), H^(2^i) i < 7 after.
-constexpr uint32_t kKsRows = 65536u;
-constexpr uint32_t kKsSbox = 131072u;
+// LDS (dynamic only: offsets are addresses): AES row image @0 (64 KiB), S-box bytes @64K
+// (256 words), then 8 slots: H^(2^i) for i < 7 and H^3 (slot 7).
+constexpr uint32_t kKsRows = 0u;
+constexpr uint32_t kKsSbox = 65536u;
 constexpr uint32_t kKsPow = kKsSbox + 1024u;
 constexpr uint32_t kKsLds = kKsPow + 8u * 16u;
 
-// One workgroup: key schedule of K' (= AES_K(V) in mode 1), H = E_K'(0), H^(2^i) by 31 table
-// squarings (the squaring map is GF(2)-linear: 16 LDS lookups each, no 128-step shift chain),
-// H^3 by one generic multiply, and the basis chains the table kernel expands.
+// bit k (coefficient of x^k) of a memory-order element
+__device__ __forceinline__ uint32_t gf_bit(u32x4 x, uint32_t k) {
+  return (x[k >> 5] >> (8u * ((k >> 3) & 3u) + 7u - (k & 7u))) & 1u;
+}
+
+// One workgroup of 256: key schedule of K' (= AES_K(V) in mode 1), H = E_K'(0); then, with no
+// serial chain longer than one step: H^(2^i), i = 1..31, as XORs of the columns of the squaring
+// maps (8 threads per i, 16 columns each); H^3 = H^2 · H by one wave (lane q holds H·x^q and
+// H·x^(q+64)); and the basis chains P · x^i of the 8 multipliers, one gf_mulx_pow per entry.
 __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
-  stage_copy(a.sqtab, 0u, 4096u);
   stage_rows(a.te0, kKsRows);
   for (uint32_t x = threadIdx.x; x < 256u; x += blockDim.x) lds_st32(kKsSbox + 4u * x, (a.te0[x] >> 8) & 0xffu);
   __syncthreads();
@@ -70,39 +76,60 @@ __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
   uint32_t h0 = 0u, h1 = 0u, h2 = 0u, h3 = 0u;
   aes128_enc(fk, rl, h0, h1, h2, h3);  // H = E_K'(0^128)
   const u32x4 H = u32x4{h0, h1, h2, h3};
-  if (threadIdx.x < 44u) a.keys[threadIdx.x] = fk.w[threadIdx.x];
-  if (threadIdx.x == 0) {
+  const uint32_t t = threadIdx.x;
+  if (t < 44u) a.keys[t] = fk.w[t];
+  if (t == 0u) {
     a.keys[48] = h0;
     a.keys[49] = h1;
     a.keys[50] = h2;
     a.keys[51] = h3;
+    a.h2pow[0] = H;
+    lds_st128(kKsPow, H);
   }
-  // H^(2^i) by squaring (every lane of wave 0 redundantly; lane 0 stores)
-  if (threadIdx.x < 64u) {
-    const GhashLane gl = ghash_lane();
-    u32x4 p = H;
-    for (uint32_t i = 0; i < 32u; ++i) {
-      if (threadIdx.x == 0) {
-        a.h2pow[i] = p;
-        if (i < 7u) lds_st128(kKsPow + 16u * i, p);  // the chained multipliers H^(2^i), i < 7
-      }
-      p = gmul_byte(p, gl);  // p^2
+  // H^(2^i) = Sq^i(H) = XOR over the set bits k of H of column k of Sq^i
+  if (t < 248u) {
+    const uint32_t i = 1u + (t >> 3), k0c = 16u * (t & 7u);
+    const u32x4* col = a.sqmat + (i - 1u) * 128u + k0c;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t c = 0; c < 16u; ++c) {
+      const u32x4 v = col[c];
+      if (gf_bit(H, k0c + c)) acc ^= v;
+    }
+    acc ^= shfl_xor4(acc, 1);
+    acc ^= shfl_xor4(acc, 2);
+    acc ^= shfl_xor4(acc, 4);
+    if ((t & 7u) == 0u) {
+      a.h2pow[i] = acc;
+      if (i < 7u) lds_st128(kKsPow + 16u * i, acc);
     }
   }
   __syncthreads();
-  // basis chains: lane j < 8 walks P_j through P_j · x^i, i = 0..127
-  if (threadIdx.x < 8u) {
-    const uint32_t j = threadIdx.x;
-    const u32x4 P = j == 2 ? gmul_generic32(lds128(kKsPow + 16u), lds128(kKsPow))  // H^3
-                           : lds128(kKsPow + 16u * (j < 2u ? j : j - 1u));       // H, H^2, H^4 .. H^64
+  // H^3 = H^2 · H: lane q contributes H·x^q [bit q of H^2] and H·x^(q+64) [bit q+64]
+  if (t < 64u) {
+    const u32x4 H2 = lds128(kKsPow + 16u);
+    uint64_t ah, al, bh, bl;
+    gf_split(H, ah, al);
+    bh = ah;
+    bl = al;
+    gf_mulx_pow(ah, al, t);
+    gf_mulx_pow(bh, bl, t + 64u);
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    if (gf_bit(H2, t)) acc ^= gf_join(ah, al);
+    if (gf_bit(H2, t + 64u)) acc ^= gf_join(bh, bl);
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) acc ^= shfl_xor4(acc, m);
+    if (t == 0u) lds_st128(kKsPow + 16u * 7u, acc);
+  }
+  __syncthreads();
+  // basis chains: entry (j, i) = P_j · x^i, P_j = H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
+  for (uint32_t e = t; e < 1024u; e += blockDim.x) {
+    const uint32_t j = e >> 7, i = e & 127u;
+    const uint32_t slot = j == 2u ? 7u : (j < 2u ? j : j - 1u);
     uint64_t ph, pl;
-    gf_split(P, ph, pl);
-    for (uint32_t i = 0; i < 128u; ++i) {
-      a.chains[j * 128u + i] = gf_join(ph, pl);
-      const uint64_t lsb = 0 - (pl & 1u);
-      pl = (pl >> 1) | (ph << 63);
-      ph = (ph >> 1) ^ (0xE100000000000000ULL & lsb);
-    }
+    gf_split(lds128(kKsPow + 16u * slot), ph, pl);
+    gf_mulx_pow(ph, pl, i);
+    a.chains[e] = gf_join(ph, pl);
   }
 }
 
