@@ -340,6 +340,7 @@ int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size
 // 2 = "0000000"||flag||BE32(ctr0 + r) with the prefix written, 3 = fixed 12 bytes.
 struct NonceSpec {
   uint32_t mode = 0, ctr0 = 0, flag = 0;
+  uint32_t flag2 = 0, flag2_from = 0xFFFFFFFFu;  // mode 2: records >= flag2_from carry flag2
   uint32_t fix[3] = {0, 0, 0};
 };
 
@@ -384,6 +385,8 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.nmode = ns.mode;
   a.nctr0 = ns.ctr0;
   a.nflag = ns.flag;
+  a.nflag2 = ns.flag2;
+  a.nflag2_from = ns.flag2_from;
   memcpy(a.nfix, ns.fix, sizeof a.nfix);
   a.sched = (uint32_t)g_sched.load();
   if (p.wide) {

@@ -72,13 +72,20 @@ int run_602(const cmpi_ctx* c, const cmpi_602_plan& p, const uint8_t header[25],
   const bool small = p.mode == '1' && p.total <= k602Pipe;
   size_t i = 0;
   while (i < segs.size()) {
-    size_t j = i + 1;
+    // one batch per run of equal-length segments at uniform pitches; the sender's flag byte may
+    // change once inside a run (the last outer message's segments carry '1', send.c:779-799),
+    // the receiver reads it from the wire
+    size_t j = i + 1, split = 0;
     if (!small && j < segs.size()) {
       const uint64_t dp = segs[j].pt_off - segs[i].pt_off, dw = segs[j].wire_off - segs[i].wire_off;
-      while (j < segs.size() && segs[j].len == segs[i].len && segs[j].flag == segs[i].flag &&
-             segs[j].ctr == segs[i].ctr + (j - i) && segs[j].pt_off == segs[i].pt_off + dp * (j - i) &&
-             segs[j].wire_off == segs[i].wire_off + dw * (j - i))
+      while (j < segs.size() && segs[j].len == segs[i].len && segs[j].ctr == segs[i].ctr + (j - i) &&
+             segs[j].pt_off == segs[i].pt_off + dp * (j - i) && segs[j].wire_off == segs[i].wire_off + dw * (j - i)) {
+        if (!DEC && segs[j].flag != segs[j - 1].flag) {
+          if (split) break;
+          split = j - i;
+        }
         ++j;
+      }
     }
     const Seg602& s0 = segs[i];
     const size_t nrec = j - i;
@@ -92,6 +99,10 @@ int run_602(const cmpi_ctx* c, const cmpi_602_plan& p, const uint8_t header[25],
       ns.mode = DEC ? 1 : 2;
       ns.ctr0 = s0.ctr;
       ns.flag = s0.flag;
+      if (split) {
+        ns.flag2 = segs[i + split].flag;
+        ns.flag2_from = (uint32_t)split;
+      }
     }
     int rc;
     if (!DEC) {

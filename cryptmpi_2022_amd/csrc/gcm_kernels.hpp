@@ -44,13 +44,14 @@ struct GcmArgs {
   //  0: 12 bytes at nonces + r*nonce_stride
   //  1: "0000000" || the 5-byte segment prefix at nonces + r*nonce_stride   (602 receiver,
   //     recv.c:594-609 / :749-764 rebuilds the nonce from the wire)
-  //  2: "0000000" || nflag || BE32(nctr0 + r); seal also writes that 5-byte prefix at
+  //  2: "0000000" || flag || BE32(nctr0 + r), flag = nflag (records r < nflag2_from) or
+  //     nflag2 (r >= nflag2_from: the last outer message's segments); seal also writes that 5-byte prefix at
   //     nonces + r*nonce_stride                                              (602 sender,
   //     send.c:651-670 / :779-799)
   //  3: the 12 bytes nfix[] for every record; seal also writes them at nonces + r*nonce_stride
   //     when nonces != null                                                  (600 sender, one
   //     RAND_bytes nonce per message, send.c:294-311)
-  uint32_t nmode, nctr0, nflag;
+  uint32_t nmode, nctr0, nflag, nflag2, nflag2_from;
   uint32_t nfix[3];
   // wide decomposition (gcm_wide_kernel): S steps per chunk, nch chunks per record, and the
   // nibble tables of H^(2^b), b = 0..6 (lane weights)
@@ -99,7 +100,7 @@ __device__ __forceinline__ void gcm_nonce(const GcmArgs& a, uint32_t r, bool wri
       f = nb8[0];
       c = ((uint32_t)nb8[1] << 24) | ((uint32_t)nb8[2] << 16) | ((uint32_t)nb8[3] << 8) | nb8[4];
     } else {
-      f = a.nflag;
+      f = r >= a.nflag2_from ? a.nflag2 : a.nflag;
       c = a.nctr0 + r;
       if (writer) {
         nb8[0] = (uint8_t)f;
