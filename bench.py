@@ -174,6 +174,30 @@ def aggregate(wall: float, per_rank_bytes: int, steps: int, pg, device) -> tuple
     return wall_max, per_rank_bytes * ws * steps / wall_max / GIB
 
 
+# The binding on-chip resource of the GCM kernels is the LDS array (DESIGN.md "Roofline"): per
+# 16-B counter block 133 ds_read_b32 T-table lookups (rounds 1-2 counter-cached: 1 + 4, rounds 3-9
+# 7 x 16, last 16) at 2 LDS cycles per wave-instruction, and per GHASH block 16 ds_read_b128
+# byte-table lookups at 4 (MI355X_MICROARCH.md "LDS": 64 banks, lane groups per instruction).
+LDS_CLK_HZ = 2.4e9  # MI355X peak engine clock
+AES_B32_LOOKUPS, GHASH_B128_LOOKUPS = 133, 16
+
+
+def lds_roofline(w, kern_ms: float, device: int) -> dict:
+    """LDS-array cycles the GCM seal launch needs at minimum (AES of nb data blocks + J0, GHASH of
+    nb blocks + the length block, per record) against ncu x clock x kernel time."""
+    import torch
+
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    nb = (w.n + 15) // 16
+    per_block = (AES_B32_LOOKUPS * 2 + GHASH_B128_LOOKUPS * 4) / 64.0  # LDS cycles per block per CU
+    cycles = w.nrec * (nb + 1) * per_block
+    avail = kern_ms * 1e-3 * ncu * LDS_CLK_HZ
+    return {"bound": "lds", "unit": "Gblock/s", "cycles_per_block": round(per_block, 3),
+            "achieved": round(w.nrec * (nb + 1) / (kern_ms * 1e-3) / 1e9, 2),
+            "peak": round(ncu * LDS_CLK_HZ / per_block / 1e9, 2), "frac": round(cycles / avail, 4),
+            "note": "AES 133 ds_read_b32 + GHASH 16 ds_read_b128 per 16-B block; J0 and length block counted"}
+
+
 def copy_peak_gbs(device: int, nbytes: int = 1 << 30, reps: int = 10) -> float:
     """Achievable HBM bandwidth on this box: device-to-device copy of 1 GiB (read + write bytes
     / time, best of `reps`) — the 'measured copy-kernel peak' of BASELINE.md §3."""
@@ -462,6 +486,7 @@ def main() -> None:
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "seal launch (gcm_batch_kernel<L,false>)" if w.alg == "gcm" else f"{w.alg} seal launch",
                      "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bpl},
+        "lds_roofline": lds_roofline(w, kern_ms, local) if w.alg == "gcm" else None,
         "verified_round_trip": ok,
     }
     w.free()

@@ -20,9 +20,25 @@ res = {}
 for wl in sys.argv[3:]:
     w = Workload(wl, 0, seed=3)
     t = {(v, op): [] for v in values for op in ("seal", "open")}
+    alt = os.environ.get("ABK_ALT") == "1"  # bench.py's timing: seal/open alternating per step
     for rnd in range(7):
         for v in values:
             setter(v)
+            if alt:
+                w.seal()
+                w.open()
+                torch.cuda.synchronize()
+                ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(4)]
+                for e0, e1, e2 in ev:
+                    e0.record()
+                    w.seal()
+                    e1.record()
+                    w.open()
+                    e2.record()
+                torch.cuda.synchronize()
+                t[(v, "seal")].append(sum(a.elapsed_time(b) for a, b, _ in ev) / 4)
+                t[(v, "open")].append(sum(b.elapsed_time(c) for _, b, c in ev) / 4)
+                continue
             for op in ("seal", "open"):
                 fn = w.seal if op == "seal" else w.open
                 fn()
