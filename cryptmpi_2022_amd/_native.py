@@ -93,6 +93,7 @@ _SIGS = {
     "cmpi_debug_force_plan": ([_I, _U32], None),
     "cmpi_debug_force_wide": ([_I, _U32], None),
     "cmpi_debug_set_gcm_prefetch": ([_I], None),
+    "cmpi_debug_set_wide_chw": ([_I], None),
     "cmpi_debug_set_wide_probe": ([_P], None),
     "cmpi_debug_set_ctr_lds": ([_I], None),
     "cmpi_debug_set_gcm_ablation": ([_I], None),

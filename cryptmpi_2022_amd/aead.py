@@ -206,6 +206,12 @@ def force_wide(mode: int = 0, steps: int = 0) -> None:
     N.lib().cmpi_debug_force_wide(mode, steps)
 
 
+def set_wide_chw(on: bool = True) -> None:
+    """Test hook: wide GCM plan applies the chunk weights in the wide kernel (True, default) or in
+    the combine kernel (False)."""
+    N.lib().cmpi_debug_set_wide_chw(1 if on else 0)
+
+
 def gcm_plan(ctx: AeadCtx, length: int, nrec: int):
     out = (ctypes.c_uint32 * 4)()
     N.check(N.lib().cmpi_debug_gcm_plan(ctx.handle, length, nrec, out))

@@ -473,6 +473,33 @@ __device__ __forceinline__ u32x4 shfl_xor4(u32x4 v, int m) {
   return r;
 }
 
+// Y · M for wave-uniform Y and M, computed by the whole wavefront (all 64 lanes active):
+// Y·M = XOR_k m_k · (Y·x^k); lane l takes the coefficients k = 2l, 2l+1 of M (one variable
+// shift gf_mulx_pow and one single shift), and the 64 lane terms are XOR-reduced with
+// shuffles.  ~70 VALU per lane — one generic product where a single lane would need ~1.4 k.
+// Every lane returns the product.
+__device__ __forceinline__ u32x4 gmul_wave(u32x4 y, u32x4 m) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t yh, yl, mh, ml;
+  gf_split(y, yh, yl);
+  gf_split(m, mh, ml);
+  const uint32_t k = 2u * lane;  // coefficient of x^k sits at bit 127 - k of (mh:ml)
+  const uint64_t mw = lane < 32u ? mh : ml;
+  const uint32_t kk = k & 63u;
+  const uint64_t b0 = 0 - ((mw >> (63u - kk)) & 1u), b1 = 0 - ((mw >> (62u - kk)) & 1u);
+  gf_mulx_pow(yh, yl, k);
+  uint64_t zh = yh & b0, zl = yl & b0;
+  const uint64_t lsb = 0 - (yl & 1u);
+  yl = (yl >> 1) | (yh << 63);
+  yh = (yh >> 1) ^ (0xE100000000000000ULL & lsb);
+  zh ^= yh & b1;
+  zl ^= yl & b1;
+  u32x4 z = gf_join(zh, zl);
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) z ^= shfl_xor4(z, s);
+  return z;
+}
+
 // Partial-block helpers (bytes [0, n) of a 16-byte block at an arbitrary address).
 __device__ __forceinline__ u32x4 load_partial(const uint8_t* p, uint32_t n) {
   uint32_t b[16];

@@ -129,6 +129,8 @@ struct cmpi_ctx {
   // per-G combine multipliers H^{G·2^j}, j < 7 (host-keyed contexts; passed by value)
   mutable std::mutex mu;
   mutable std::map<uint32_t, std::array<Blk, 7>> mj;
+  // wide-plan chunk weights H^(1 + (nch-1-i)·C) in HBM, per (C, nch) (host-keyed contexts)
+  mutable std::map<std::pair<uint32_t, uint32_t>, void*> chw;
   // internal scratch (partials, status) and staging for *_host
   mutable void* scratch = nullptr;
   mutable size_t scratch_cap = 0;
@@ -186,7 +188,8 @@ struct GcmPlan {
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
-std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4/6
+std::atomic<int> g_gcm_pf{2};
+std::atomic<int> g_wide_chw{1};       // wide plan: chunk weights in the wide kernel (1) or the combine (0)         // GCM input prefetch depth (slots), 2/3/4/6
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
 std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
@@ -297,6 +300,33 @@ int get_mj(const cmpi_ctx* c, uint32_t G, cmpi::dev::GcmCombineArgs& ca) {
   return CMPI_OK;
 }
 
+// Chunk weights of the wide plan, W_i = H^(1 + (nch-1-i)·C), i < nch (gcm_wide_kernel applies
+// W_i to chunk i's lane-weighted sum, so the combine only XORs): built on the host from H once
+// per (C, nch) and kept in HBM for the context's lifetime.  Device-keyed contexts (no host H)
+// return null and keep the combine kernel's Horner weighting.
+int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out) {
+  *out = nullptr;
+  if (c->dev_keys) return CMPI_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  auto key = std::make_pair(C, nch);
+  auto it = c->chw.find(key);
+  if (it == c->chw.end()) {
+    std::vector<Blk> w(nch);
+    const Blk P = cmpi::gf_pow(c->H, C);
+    w[nch - 1] = c->H;
+    for (uint32_t i = nch - 1; i-- > 0;) w[i] = cmpi::gf_mul(w[i + 1], P);
+    void* d = nullptr;
+    if (hipMalloc(&d, (size_t)nch * 16) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc chunk weights failed");
+    if (hipMemcpy(d, w.data(), (size_t)nch * 16, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(d);
+      return fail(CMPI_EHIP, "chunk weights copy failed");
+    }
+    it = c->chw.emplace(key, d).first;
+  }
+  *out = reinterpret_cast<const u32x4*>(it->second);
+  return CMPI_OK;
+}
+
 template <bool DEC>
 int launch_gcm_combine(const cmpi_ctx* c, cmpi::dev::GcmCombineArgs& ca, uint32_t G, hipStream_t st) {
   int rc = get_mj(c, G, ca);
@@ -404,6 +434,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.nch = p.nseg;
     int rc = get_h64tab(c, &a.htab);
     if (!rc) rc = get_wnib(c, &a.wtab);
+    if (!rc && g_wide_chw.load() && !(a.sched & 8u)) rc = get_chw(c, p.G, p.nseg, &a.chw);
     if (rc) return rc;
     a.probe = g_wide_probe.load();
     auto fn = cmpi::dev::gcm_wide_kernel<DEC>;
@@ -424,8 +455,9 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     ca.nrec = (uint32_t)nrec;
     ca.nseg = p.nseg;
     ca.partial = a.partial;
-    ca.ekj0 = a.ekj0;
+    ca.ekj0 = a.chw ? nullptr : a.ekj0;
     ca.status = status;
+    ca.prew = a.chw ? 1u : 0u;
     return launch_gcm_combine<DEC>(c, ca, p.G, st);  // chunk i weighted by H^{(nch-1-i)·64S}, as segments
   }
   if (p.nseg > 1) {
@@ -951,6 +983,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   // scratch and staging go back to the allocator.
   (void)hipDeviceSynchronize();
   if (c->scratch) (void)hipFree(c->scratch);
+  for (auto& kv : c->chw) (void)hipFree(kv.second);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
   if (c->pipe) {
@@ -999,6 +1032,7 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
   g_force_nseg.store(segments);
 }
 
+void cmpi_debug_set_wide_chw(int on) { g_wide_chw.store(on ? 1 : 0); }
 void cmpi_debug_set_wide_probe(void* buf) { g_wide_probe.store(reinterpret_cast<uint64_t*>(buf)); }
 
 void cmpi_debug_set_gcm_prefetch(int slots) { g_gcm_pf.store(slots == 3 || slots == 4 || slots == 6 ? slots : 2); }

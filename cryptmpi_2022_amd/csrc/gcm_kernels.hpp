@@ -57,6 +57,9 @@ struct GcmArgs {
   // nibble tables of H^(2^b), b = 0..6 (lane weights)
   const u32x4* wtab;
   uint32_t S, nch;
+  // host-keyed contexts: chunk weights chw[i] = H^(1 + (nch-1-i)·64S) (gcm_wide_kernel applies
+  // them itself, chunk 0 adds E_K(J0): the combine only XORs); null = weighted in the combine
+  const u32x4* chw;
   uint64_t* probe;  // diagnostics (cmpi_debug_set_wide_probe): per-WG phase timestamps, or null
   RoundKeys rk;
 };
@@ -334,6 +337,7 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
     __syncthreads();
     if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 1u] = wall_clock64();
     u32x4 acc = {0u, 0u, 0u, 0u};
+    u32x4 ekj = {0u, 0u, 0u, 0u};
     if (active) {
       const uint32_t r = u / a.nch;
       const uint32_t i = u - r * a.nch;
@@ -394,9 +398,10 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
         if (k + 1u < steps) consume(k + 1u, vb);
         vb = prefetch(k + 3u);
       }
-      if (i == 0u) {  // E_K(J0) for the combine kernel
+      if (i == 0u) {  // E_K(J0): into chunk 0's partial, or for the combine kernel
         const u32x4 e = keystream(1u);
-        if (lane == 0u) a.ekj0[r] = e;
+        if (a.chw) ekj = e;
+        else if (lane == 0u) a.ekj0[r] = e;
       }
     }
     if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 2u] = wall_clock64();
@@ -426,7 +431,16 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
           acc = gmul_nib(acc, b * 8192u) ^ up;
         }
       }
-      if (lane == 0u) a.partial[u] = gmul_nib(acc, 0u);
+      if (a.chw) {
+        // lane 0 holds XOR_q acc_q · H^(63-q); times the chunk weight H^(1 + (nch-1-i)·64S)
+        // by the whole wave (wave-uniform operands), plus E_K(J0) in chunk 0
+        const u32x4 y = {(uint32_t)__builtin_amdgcn_readfirstlane(acc[0]), (uint32_t)__builtin_amdgcn_readfirstlane(acc[1]),
+                         (uint32_t)__builtin_amdgcn_readfirstlane(acc[2]), (uint32_t)__builtin_amdgcn_readfirstlane(acc[3])};
+        const u32x4 pw = gmul_wave(y, a.chw[u % a.nch]) ^ ekj;
+        if (lane == 0u) a.partial[u] = pw;
+      } else if (lane == 0u) {
+        a.partial[u] = gmul_nib(acc, 0u);
+      }
     }
     if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 5u] = wall_clock64();
   }
@@ -446,6 +460,7 @@ struct GcmCombineArgs {
   int32_t* status;
   const u32x4* mjp;      // device-keyed: M_j = H^{G·2^j} = H^(2^(log2 G + j)) in HBM, j < 7; or null:
   u32x4 mjv[7];          // host-keyed: M_j by value
+  uint32_t prew;         // partials already weighted, E_K(J0) included (wide plan, chw): XOR only
 };
 
 // One wave per record: Y = XOR_s partial[s] · H^{(nseg-1-s)·G}; tag = Y ^ E_K(J0).
@@ -460,7 +475,7 @@ constexpr size_t kCombineLds = 7u * 8192u;
 template <bool DECRYPT>
 __global__ __launch_bounds__(256) void gcm_combine_kernel(GcmCombineArgs a) {
   const uint32_t nseg = a.nseg;
-  const uint32_t nt = nseg > 64u ? 7u : nseg > 1u ? 32u - __builtin_clz(nseg - 1u) : 0u;
+  const uint32_t nt = a.prew ? 0u : nseg > 64u ? 7u : nseg > 1u ? 32u - __builtin_clz(nseg - 1u) : 0u;
   const uint32_t t = threadIdx.x, lane = t & 63u;
   if (t < nt * 32u) {
     const uint32_t j = t >> 5;
@@ -477,16 +492,20 @@ __global__ __launch_bounds__(256) void gcm_combine_kernel(GcmCombineArgs a) {
   for (uint32_t r = blockIdx.x * wpb + (t >> 6); r < a.nrec; r += gridDim.x * wpb) {
     const u32x4* part = a.partial + (uint64_t)r * nseg;
     u32x4 y = {0u, 0u, 0u, 0u};
-    for (uint32_t m = mmax; m-- > 0u;) {
-      if (m + 1u < mmax) y = gmul_nib(y, 6u * 8192u);
-      const uint32_t k = lane + 64u * m;
-      if (k < nseg) y ^= part[nseg - 1u - k];
-    }
+    if (a.prew) {
+      for (uint32_t k = lane; k < nseg; k += 64u) y ^= part[k];
+    } else {
+      for (uint32_t m = mmax; m-- > 0u;) {
+        if (m + 1u < mmax) y = gmul_nib(y, 6u * 8192u);
+        const uint32_t k = lane + 64u * m;
+        if (k < nseg) y ^= part[nseg - 1u - k];
+      }
 #pragma unroll
-    for (uint32_t j = 0; j < 6u; ++j) {
-      if ((1u << j) >= nseg) break;  // wave-uniform: lane < nseg needs only bits j < nt
-      const u32x4 q = gmul_nib(y, j * 8192u);
-      if ((lane >> j) & 1u) y = q;
+      for (uint32_t j = 0; j < 6u; ++j) {
+        if ((1u << j) >= nseg) break;  // wave-uniform: lane < nseg needs only bits j < nt
+        const u32x4 q = gmul_nib(y, j * 8192u);
+        if ((lane >> j) & 1u) y = q;
+      }
     }
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) y ^= shfl_xor4(y, m);

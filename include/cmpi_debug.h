@@ -37,6 +37,9 @@ void cmpi_debug_set_wide_probe(void* buf);
  * records): mode 0 automatic, 1 always when legal (host-keyed context, >= 64 data blocks),
  * -1 never; steps per chunk (0 = automatic). */
 void cmpi_debug_force_wide(int mode, uint32_t steps);
+/* Wide GCM plan, host-keyed contexts: 1 = chunk weights applied in gcm_wide_kernel, the combine
+   only XORs (default); 0 = weights applied by the combine kernel (Horner in H^(64S·64)). */
+void cmpi_debug_set_wide_chw(int on);
 /* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}; a wide plan reports
  * L = 64, nseg = chunks per record, G = X-blocks per chunk (64*steps). */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);

@@ -27,6 +27,7 @@ def _auto_plan():
     yield
     aead.force_plan(0, 0)
     aead.force_wide(0, 0)
+    aead.set_wide_chw(True)
 
 
 def gpu_seal(ctx, nonces: np.ndarray, pt: np.ndarray) -> np.ndarray:
@@ -174,11 +175,14 @@ def test_large_records_multisegment():
 
 @pytest.mark.parametrize("n,nrec,steps", [(1024, 3, 1), (1040, 2, 1), (4097, 3, 2), (65535, 2, 4), (100000, 3, 3),
                                           (1 << 20, 2, 0), (64 * 16 * 5 - 16, 2, 5)])
-def test_wide_decomposition(n, nrec, steps):
+@pytest.mark.parametrize("chw", [True, False])
+def test_wide_decomposition(n, nrec, steps, chw):
     """Wide plan (one wave per 64*steps-block chunk; chunk 0 takes the remainder, G <= r0 < 2G
-    or the whole record; lane-weighted partials): bit-exact seal, round trip, forged record
-    zero-filled, unaligned wire layout."""
+    or the whole record; lane-weighted partials; chunk weights applied in the wide kernel by a
+    wave-cooperative multiply, or by the combine kernel): bit-exact seal, round trip, forged
+    record zero-filled, unaligned wire layout."""
     aead.force_wide(1, steps)
+    aead.set_wide_chw(chw)
     ctx = aead.AeadCtx(KEY)
     L, nch, G, r0 = aead.gcm_plan(ctx, n, nrec)
     nx = n // 16 + (n % 16 > 0) + 1

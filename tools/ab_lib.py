@@ -45,7 +45,7 @@ for spec in args.libs:  # path[:sched] — the same .so may be loaded twice unde
 dev = torch.device("cuda:0")
 key = bytes(range(16))
 SHAPES = {"gcm1k": ("gcm", 65536, 1024), "gcm4k": ("gcm", 65536, 4096), "ocb1m": ("ocb", 4096, 1 << 20),
-          "ctr1g": ("ctr", 1, 1 << 30)}
+          "ctr1g": ("ctr", 1, 1 << 30), "a2a": ("gcm", 8, 1 << 20), "a2a64": ("gcm", 64, 1 << 20)}
 
 
 def ptr(t):
