@@ -134,41 +134,58 @@ class Workload:
         torch.cuda.empty_cache()
 
 
-EVENT_STRIDE = 4  # per-kernel HIP events on every 4th timed step (event packets cost ~1 us each)
+class KernelEvents:
+    """HIP events recorded on the launch stream around every seal and open of the timed region,
+    created with hipEventDisableSystemFence (the library's cmpi_debug_event_*): a default event
+    (torch.cuda.Event) performs a system-scope fence — cache writeback + invalidate — that left a
+    ~6 us bubble before each following launch (rocprofv3 kernel trace)."""
+
+    def __init__(self, n: int):
+        from cryptmpi_2022_amd import _native as N
+
+        self.L = N.lib()
+        self.ev = [self.L.cmpi_debug_event_new() for _ in range(n)]
+        assert all(self.ev), "hipEventCreateWithFlags failed"
+
+    def record(self, i: int, stream) -> None:
+        assert self.L.cmpi_debug_event_record(self.ev[i], stream) == 0
+
+    def ms(self, i: int, j: int) -> float:
+        t = self.L.cmpi_debug_event_ms(self.ev[i], self.ev[j])
+        assert t >= 0.0, "hipEventElapsedTime failed"
+        return t
+
+    def free(self) -> None:
+        for e in self.ev:
+            self.L.cmpi_debug_event_free(e)
 
 
 def time_steps(w: Workload, steps: int, warmup: int, barrier):
     """Returns (wall seconds for `steps` steps, avg seal kernel ms, avg open kernel ms) —
-    kernel times from HIP events recorded on the stream the kernels are launched on, around the
-    seal and open launches of every EVENT_STRIDE-th step of the timed region."""
+    kernel times from HIP events recorded on the stream the kernels are launched on, around every
+    seal and open launch of the timed region (fence-free events, KernelEvents)."""
     for _ in range(warmup):
         w.seal()
         w.open()
     torch.cuda.synchronize(w.dev)
     assert w.verify(), "round trip failed in warm-up"
-    stream = torch.cuda.current_stream(w.dev)
-    timed = set(range(0, steps, EVENT_STRIDE))
-    ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-              torch.cuda.Event(enable_timing=True)) for i in timed}
+    stream = torch.cuda.current_stream(w.dev).cuda_stream
+    ev = KernelEvents(2 * steps + 1)
     barrier()
     torch.cuda.synchronize(w.dev)
     t0 = time.perf_counter()
+    ev.record(0, stream)
     for i in range(steps):
-        if i in timed:
-            e0, e1, e2 = ev[i]
-            e0.record(stream)
-            w.seal()
-            e1.record(stream)
-            w.open()
-            e2.record(stream)
-        else:
-            w.seal()
-            w.open()
+        w.seal()
+        ev.record(2 * i + 1, stream)
+        w.open()
+        ev.record(2 * i + 2, stream)
     torch.cuda.synchronize(w.dev)
     barrier()
     wall = time.perf_counter() - t0
-    seal_ms = sum(a.elapsed_time(b) for a, b, _ in ev.values()) / len(ev)
-    open_ms = sum(b.elapsed_time(c) for _, b, c in ev.values()) / len(ev)
+    seal_ms = sum(ev.ms(2 * i, 2 * i + 1) for i in range(steps)) / steps
+    open_ms = sum(ev.ms(2 * i + 1, 2 * i + 2) for i in range(steps)) / steps
+    ev.free()
     return wall, seal_ms, open_ms
 
 

@@ -1033,6 +1033,26 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
 }
 
 void cmpi_debug_set_wide_chw(int on) { g_wide_chw.store(on ? 1 : 0); }
+
+// Timing events without the system-scope release fence (hipEventDisableSystemFence): a default
+// event's fence writes back and invalidates the caches and leaves a ~6 us bubble before the
+// next launch — the bench times kernels with these instead.
+void* cmpi_debug_event_new(void) {
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
+  return e;
+}
+int cmpi_debug_event_record(void* ev, void* stream) {
+  return hipEventRecord((hipEvent_t)ev, (hipStream_t)stream) == hipSuccess ? CMPI_OK : CMPI_EHIP;
+}
+float cmpi_debug_event_ms(void* a, void* b) {
+  float ms = -1.0f;
+  if (hipEventElapsedTime(&ms, (hipEvent_t)a, (hipEvent_t)b) != hipSuccess) return -1.0f;
+  return ms;
+}
+void cmpi_debug_event_free(void* ev) {
+  if (ev) (void)hipEventDestroy((hipEvent_t)ev);
+}
 void cmpi_debug_set_wide_probe(void* buf) { g_wide_probe.store(reinterpret_cast<uint64_t*>(buf)); }
 
 void cmpi_debug_set_gcm_prefetch(int slots) { g_gcm_pf.store(slots == 3 || slots == 4 || slots == 6 ? slots : 2); }

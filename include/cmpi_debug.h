@@ -40,6 +40,13 @@ void cmpi_debug_force_wide(int mode, uint32_t steps);
 /* Wide GCM plan, host-keyed contexts: 1 = chunk weights applied in gcm_wide_kernel, the combine
    only XORs (default); 0 = weights applied by the combine kernel (Horner in H^(64S·64)). */
 void cmpi_debug_set_wide_chw(int on);
+/* Kernel timing (bench.py): HIP events created with hipEventDisableSystemFence (no cache
+   writeback/invalidate when recorded).  event_ms: elapsed ms between two recorded events after
+   the stream has been synchronised, -1 on error. */
+void* cmpi_debug_event_new(void);
+int cmpi_debug_event_record(void* ev, void* stream);
+float cmpi_debug_event_ms(void* a, void* b);
+void cmpi_debug_event_free(void* ev);
 /* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}; a wide plan reports
  * L = 64, nseg = chunks per record, G = X-blocks per chunk (64*steps). */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);
