@@ -500,6 +500,34 @@ __device__ __forceinline__ u32x4 gmul_wave(u32x4 y, u32x4 m) {
   return z;
 }
 
+// XOR of four products Y_j · M_j (all wave-uniform), by the whole wavefront as gmul_wave with one
+// shared shuffle reduction.  Every lane returns the sum.
+__device__ __forceinline__ u32x4 gmul_wave4(const u32x4 (&y)[4], const u32x4 (&m)[4]) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t k = 2u * lane, kk = k & 63u;
+  uint64_t zh = 0, zl = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint64_t yh, yl, mh, ml;
+    gf_split(y[j], yh, yl);
+    gf_split(m[j], mh, ml);
+    const uint64_t mw = lane < 32u ? mh : ml;
+    const uint64_t b0 = 0 - ((mw >> (63u - kk)) & 1u), b1 = 0 - ((mw >> (62u - kk)) & 1u);
+    gf_mulx_pow(yh, yl, k);
+    zh ^= yh & b0;
+    zl ^= yl & b0;
+    const uint64_t lsb = 0 - (yl & 1u);
+    yl = (yl >> 1) | (yh << 63);
+    yh = (yh >> 1) ^ (0xE100000000000000ULL & lsb);
+    zh ^= yh & b1;
+    zl ^= yl & b1;
+  }
+  u32x4 z = gf_join(zh, zl);
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) z ^= shfl_xor4(z, s);
+  return z;
+}
+
 // Partial-block helpers (bytes [0, n) of a 16-byte block at an arbitrary address).
 __device__ __forceinline__ u32x4 load_partial(const uint8_t* p, uint32_t n) {
   uint32_t b[16];

@@ -188,8 +188,8 @@ struct GcmPlan {
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
-std::atomic<int> g_gcm_pf{2};
-std::atomic<int> g_wide_chw{1};       // wide plan: chunk weights in the wide kernel (1) or the combine (0)         // GCM input prefetch depth (slots), 2/3/4/6
+std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4/6
+std::atomic<int> g_wide_chw{1};       // wide plan, host-keyed: barrier-free FLOW kernel with chunk weights (1) or weights in the combine (0)
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
 std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
@@ -300,10 +300,10 @@ int get_mj(const cmpi_ctx* c, uint32_t G, cmpi::dev::GcmCombineArgs& ca) {
   return CMPI_OK;
 }
 
-// Chunk weights of the wide plan, W_i = H^(1 + (nch-1-i)·C), i < nch (gcm_wide_kernel applies
-// W_i to chunk i's lane-weighted sum, so the combine only XORs): built on the host from H once
-// per (C, nch) and kept in HBM for the context's lifetime.  Device-keyed contexts (no host H)
-// return null and keep the combine kernel's Horner weighting.
+// Chunk weights of the FLOW wide kernel, chw[4i + j] = H^(49 - 16j + (nch-1-i)·C), i < nch,
+// j < 4 (the weights of chunk i's four quarter-wave sums, so the combine only XORs): built on
+// the host from H once per (C, nch) and kept in HBM for the context's lifetime.  Device-keyed
+// contexts (no host H) return null and keep the barrier-phased kernel + combine weighting.
 int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out) {
   *out = nullptr;
   if (c->dev_keys) return CMPI_OK;
@@ -311,13 +311,20 @@ int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out) {
   auto key = std::make_pair(C, nch);
   auto it = c->chw.find(key);
   if (it == c->chw.end()) {
-    std::vector<Blk> w(nch);
-    const Blk P = cmpi::gf_pow(c->H, C);
-    w[nch - 1] = c->H;
-    for (uint32_t i = nch - 1; i-- > 0;) w[i] = cmpi::gf_mul(w[i + 1], P);
+    std::vector<Blk> w((size_t)nch * 4);
+    const Blk P = cmpi::gf_pow(c->H, C), H16 = cmpi::gf_pow(c->H, 16);
+    Blk wi = c->H;  // H^(1 + (nch-1-i)·C), i = nch-1 down to 0
+    for (uint32_t i = nch; i-- > 0;) {
+      Blk q = wi;
+      for (int j = 3; j >= 0; --j) {  // j = 3: H^1·W, j = 2: H^17·W, ...
+        w[(size_t)4 * i + j] = q;
+        q = cmpi::gf_mul(q, H16);
+      }
+      wi = cmpi::gf_mul(wi, P);
+    }
     void* d = nullptr;
-    if (hipMalloc(&d, (size_t)nch * 16) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc chunk weights failed");
-    if (hipMemcpy(d, w.data(), (size_t)nch * 16, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMalloc(&d, (size_t)nch * 64) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc chunk weights failed");
+    if (hipMemcpy(d, w.data(), (size_t)nch * 64, hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipFree(d);
       return fail(CMPI_EHIP, "chunk weights copy failed");
     }
@@ -437,8 +444,8 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     if (!rc && g_wide_chw.load() && !(a.sched & 8u)) rc = get_chw(c, p.G, p.nseg, &a.chw);
     if (rc) return rc;
     a.probe = g_wide_probe.load();
-    auto fn = cmpi::dev::gcm_wide_kernel<DEC>;
-    const size_t lds = 2 * 65536;
+    auto fn = a.chw ? cmpi::dev::gcm_wide_kernel<DEC, true> : cmpi::dev::gcm_wide_kernel<DEC, false>;
+    const size_t lds = a.chw ? (size_t)cmpi::dev::kGcmNib + 4 * 8192 : 2 * 65536;
     if ((rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds))) return rc;
     const uint64_t waves = (uint64_t)nrec * p.nseg;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(

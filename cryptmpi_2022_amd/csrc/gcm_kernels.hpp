@@ -57,8 +57,8 @@ struct GcmArgs {
   // nibble tables of H^(2^b), b = 0..6 (lane weights)
   const u32x4* wtab;
   uint32_t S, nch;
-  // host-keyed contexts: chunk weights chw[i] = H^(1 + (nch-1-i)·64S) (gcm_wide_kernel applies
-  // them itself, chunk 0 adds E_K(J0): the combine only XORs); null = weighted in the combine
+  // host-keyed contexts (FLOW wide kernel): chunk weights chw[4i + j] = H^(49 - 16j + (nch-1-i)·64S)
+  // for the four quarter-wave sums of chunk i (chunk 0 adds E_K(J0): the combine only XORs)
   const u32x4* chw;
   uint64_t* probe;  // diagnostics (cmpi_debug_set_wide_probe): per-WG phase timestamps, or null
   RoundKeys rk;
@@ -307,11 +307,22 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
 // nibble tables of H^1..H^64, restaged between two workgroup barriers; AES rows at 64K.
 // (Measured, 8 x 1 MiB: this replaced one generic multiply per lane, 176 -> 202 GiB/s seal;
 // seven restaged conflict-free byte tables instead of the nibble tables were slower, 184.)
-template <bool DECRYPT>
+// FLOW (host-keyed contexts): all tables staged once — H^64 byte table [0, 64K), AES rows
+// [64K, 128K), nibble tables of H, H^2, H^4, H^8 [128K, 160K) — and no workgroup barrier after
+// that: a wave goes from its Horner loop straight to its weights.  The lane tree stops after
+// four levels (lanes 0, 16, 32, 48 hold the sums T_q of their 16 lanes, weights H^(15-t)); the
+// remaining weights H^(49-q) and the chunk weight are one wave-cooperative product per quarter
+// (gmul_wave4 with the host table chw), E_K(J0) is folded into chunk 0, the combine only XORs.
+template <bool DECRYPT, bool FLOW = false>
 __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
   const bool prb = a.probe && threadIdx.x == 0u;
   if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
   stage_rows(a.te0, kGcmRows);
+  if constexpr (FLOW) {
+    stage_copy(a.htab, 0u, 4096u);             // byte table of H^64
+    stage_copy(a.wtab, kGcmNib, 4u * 512u);     // nibble tables of H^(2^b), b = 0..3
+    __syncthreads();
+  }
 
   const RoundKeys rk = load_round_keys(a.rk, a.rkp);  // folded (host / keysetup kernel)
   const uint32_t lane = threadIdx.x & 63u;
@@ -332,9 +343,11 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
   for (uint32_t rd = 0; rd < rounds; ++rd) {
     const uint32_t u = rd * per_round + blockIdx.x * wpb + (threadIdx.x >> 6);
     const bool active = u < units;  // wave-uniform
-    __syncthreads();                // [0, 64K) is free: the previous round's weights are done
-    stage_copy(a.htab, 0u, 4096u);  // byte table of H^64
-    __syncthreads();
+    if constexpr (!FLOW) {
+      __syncthreads();                // [0, 64K) is free: the previous round's weights are done
+      stage_copy(a.htab, 0u, 4096u);  // byte table of H^64
+      __syncthreads();
+    }
     if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 1u] = wall_clock64();
     u32x4 acc = {0u, 0u, 0u, 0u};
     u32x4 ekj = {0u, 0u, 0u, 0u};
@@ -398,13 +411,36 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
         if (k + 1u < steps) consume(k + 1u, vb);
         vb = prefetch(k + 3u);
       }
-      if (i == 0u) {  // E_K(J0): into chunk 0's partial, or for the combine kernel
+      if (i == 0u) {  // E_K(J0): into chunk 0's partial (FLOW), or for the combine kernel
         const u32x4 e = keystream(1u);
-        if (a.chw) ekj = e;
+        if (FLOW) ekj = e;
         else if (lane == 0u) a.ekj0[r] = e;
       }
     }
     if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 2u] = wall_clock64();
+    if constexpr (FLOW) {
+      if (active) {
+#pragma unroll
+        for (uint32_t b = 0; b < 4u; ++b) {  // tree levels 0..3 (as below)
+          const u32x4 up = shfl_down4(acc, 1u << b);
+          if ((lane & ((2u << b) - 1u)) == 0u) {
+            asm volatile("" ::: "memory");
+            acc = gmul_nib(acc, kGcmNib + b * 8192u) ^ up;
+          }
+        }
+        u32x4 T[4], M[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) T[j][c] = (uint32_t)__builtin_amdgcn_readlane(acc[c], 16 * j);
+          M[j] = a.chw[4u * (u % a.nch) + (uint32_t)j];
+        }
+        const u32x4 pw = gmul_wave4(T, M) ^ ekj;
+        if (lane == 0u) a.partial[u] = pw;
+      }
+      if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 5u] = wall_clock64();
+      continue;
+    }
     __syncthreads();  // every wave is past its Horner loop: [0, 64K) takes the weight tables
     if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 3u] = wall_clock64();
     stage_copy(a.wtab, 0u, 7u * 512u);  // nibble tables of H^(2^b), b = 0..6, 8 KiB apart
@@ -431,16 +467,7 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
           acc = gmul_nib(acc, b * 8192u) ^ up;
         }
       }
-      if (a.chw) {
-        // lane 0 holds XOR_q acc_q · H^(63-q); times the chunk weight H^(1 + (nch-1-i)·64S)
-        // by the whole wave (wave-uniform operands), plus E_K(J0) in chunk 0
-        const u32x4 y = {(uint32_t)__builtin_amdgcn_readfirstlane(acc[0]), (uint32_t)__builtin_amdgcn_readfirstlane(acc[1]),
-                         (uint32_t)__builtin_amdgcn_readfirstlane(acc[2]), (uint32_t)__builtin_amdgcn_readfirstlane(acc[3])};
-        const u32x4 pw = gmul_wave(y, a.chw[u % a.nch]) ^ ekj;
-        if (lane == 0u) a.partial[u] = pw;
-      } else if (lane == 0u) {
-        a.partial[u] = gmul_nib(acc, 0u);
-      }
+      if (lane == 0u) a.partial[u] = gmul_nib(acc, 0u);
     }
     if (prb && rd == 0u) a.probe[blockIdx.x * 8u + 5u] = wall_clock64();
   }

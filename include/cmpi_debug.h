@@ -37,8 +37,8 @@ void cmpi_debug_set_wide_probe(void* buf);
  * records): mode 0 automatic, 1 always when legal (host-keyed context, >= 64 data blocks),
  * -1 never; steps per chunk (0 = automatic). */
 void cmpi_debug_force_wide(int mode, uint32_t steps);
-/* Wide GCM plan, host-keyed contexts: 1 = chunk weights applied in gcm_wide_kernel, the combine
-   only XORs (default); 0 = weights applied by the combine kernel (Horner in H^(64S·64)). */
+/* Wide GCM plan, host-keyed contexts: 1 = barrier-free gcm_wide_kernel<FLOW> applying the chunk
+   weights itself, the combine only XORs (default); 0 = phased kernel, weights in the combine kernel. */
 void cmpi_debug_set_wide_chw(int on);
 /* Kernel timing (bench.py): HIP events created with hipEventDisableSystemFence (no cache
    writeback/invalidate when recorded).  event_ms: elapsed ms between two recorded events after
