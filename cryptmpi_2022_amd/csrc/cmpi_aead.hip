@@ -639,7 +639,7 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
 // three streams with two staging slots:  H2D(i+1) | kernel(i) | D2H(i-1)  overlap, the slot of
 // chunk i is reused by chunk i+2 once D2H(i) completed.  Pinned host buffers (hipHostMalloc /
 // cmpi_host_register) move by DMA at PCIe rate; pageable ones are staged by the HIP runtime.
-std::atomic<size_t> g_host_chunk{(size_t)8 << 20};
+std::atomic<size_t> g_host_chunk{(size_t)16 << 20};  // 8 / 16 / 32 MiB: 30.1 / 31.2 / 30.6 GiB/s pinned (tools/host_sweep.py)
 
 // true when p lies in page-locked host memory (hipHostMalloc / hipHostRegister): it can be the
 // direct source/target of an asynchronous DMA.  Pageable memory is never handed to async copies
@@ -1027,7 +1027,7 @@ int cmpi_host_unregister(void* ptr) {
 }
 
 void cmpi_debug_set_sched(int mode) { g_sched.store(mode & 7); }
-void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)8 << 20)); }
+void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)16 << 20)); }
 void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 15); }
 
 void cmpi_debug_set_ctr_lds(int lds_bytes) {

@@ -25,7 +25,7 @@ void cmpi_debug_set_gcm_ablation(int mode);
 void cmpi_debug_set_ctr_lds(int lds_bytes);
 /* Wave-priority rotation in the main loops (default 7): bit 0 GCM, bit 1 CTR, bit 2 OCB. */
 void cmpi_debug_set_sched(int mode);
-/* Chunk bytes of the pipelined host path (*_host calls; 0 = default 8 MiB). */
+/* Chunk bytes of the pipelined host path (*_host calls; 0 = default 16 MiB). */
 void cmpi_debug_set_host_chunk(size_t bytes);
 /* GCM lane-group kernel: input prefetch depth in slots (2, 3, 4 or 6; anything else = 2). */
 void cmpi_debug_set_gcm_prefetch(int slots);
