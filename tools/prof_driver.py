@@ -15,7 +15,22 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="gcm1k")
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--seal-only", action="store_true")
+ap.add_argument("--out-stride", type=int, default=0,
+                help="gcm1k seal-only traffic calibration: output record stride (0 = dense n+16)")
 a = ap.parse_args()
+if a.out_stride:  # 65 536 x 1 KiB seals into records `out_stride` bytes apart (aligned vs dense)
+    from cryptmpi_2022_amd import aead
+
+    n, nrec = 1024, 65536
+    ctx = aead.AeadCtx(bytes(range(16)))
+    pt = torch.randint(0, 256, (nrec * n,), dtype=torch.uint8, device="cuda")
+    nn = torch.randint(0, 256, (nrec * 12,), dtype=torch.uint8, device="cuda")
+    out = torch.empty(nrec * a.out_stride, dtype=torch.uint8, device="cuda")
+    for _ in range(a.iters):
+        ctx.seal_batch(out, pt, nn, n, nrec, out_stride=a.out_stride)
+    torch.cuda.synchronize()
+    print("ok out_stride", a.out_stride)
+    sys.exit(0)
 w = Workload(a.workload, 0, seed=1)
 for _ in range(a.iters):
     w.seal()
