@@ -359,6 +359,94 @@ def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, wa
             "all_blocks_authenticated": ok}
 
 
+def config1_message(device: int, n: int = 64 << 10, iters: int = 200) -> dict:
+    """BASELINE config 1's unit of work (one 64 KiB MPI_Send/MPI_Recv message, 600 framing:
+    send.c:221-337 / recv.c:219-341) on this engine: per-message seal + open latency
+    (a) device-resident (cmpi_600_seal / cmpi_600_open, fence-free events) and (b) host-inclusive
+    from pinned memory (H2D + seal + D2H, H2D + open + D2H, synchronised per message as MPI would),
+    next to (c) OpenSSL AES-NI on one host core for the same message (the reference seals per
+    message on the CPU).  Small single messages are latency-bound on the GPU; batching is the
+    lever (config 2)."""
+    from cryptmpi_2022_amd import _native as N
+
+    dev = torch.device("cuda", device)
+    L = N.lib()
+    ctx = aead.AeadCtx(KEY, device=device)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    msg = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev)
+    payload = torch.empty(n + 28, dtype=torch.uint8, device=dev)
+    back = torch.empty(n, dtype=torch.uint8, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    nonce_buf = (ctypes.c_uint8 * 12)(*range(12))
+    nonce = ctypes.cast(nonce_buf, ctypes.c_void_p)
+    h_msg = msg.cpu().pin_memory()
+    h_payload = torch.empty(n + 28, dtype=torch.uint8).pin_memory()
+    h_back = torch.empty(n, dtype=torch.uint8).pin_memory()
+
+    def seal():
+        N.check(L.cmpi_600_seal(ctx.handle, nonce, P(payload), P(msg), n, ctypes.c_void_p(st)))
+
+    def opn():
+        N.check(L.cmpi_600_open(ctx.handle, P(back), P(payload), n, P(status), ctypes.c_void_p(st)))
+
+    for _ in range(20):
+        seal()
+        opn()
+    torch.cuda.synchronize(dev)
+    ev = KernelEvents(2 * iters + 1)
+    ev.record(0, st)
+    for i in range(iters):
+        seal()
+        ev.record(2 * i + 1, st)
+        opn()
+        ev.record(2 * i + 2, st)
+    torch.cuda.synchronize(dev)
+    seal_us = sum(ev.ms(2 * i, 2 * i + 1) for i in range(iters)) / iters * 1e3
+    open_us = sum(ev.ms(2 * i + 1, 2 * i + 2) for i in range(iters)) / iters * 1e3
+    ev.free()
+    ok = bool(status.item() == 1) and torch.equal(back, msg)
+
+    def host_msg():
+        msg.copy_(h_msg, non_blocking=True)
+        seal()
+        h_payload.copy_(payload, non_blocking=True)
+        torch.cuda.synchronize(dev)  # MPI_Send of the payload would start here
+        payload.copy_(h_payload, non_blocking=True)
+        opn()
+        h_back.copy_(back, non_blocking=True)
+        torch.cuda.synchronize(dev)
+
+    for _ in range(20):
+        host_msg()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        host_msg()
+    host_us = (time.perf_counter() - t0) / iters * 1e6
+    ok = ok and torch.equal(h_back, h_msg)
+    res = {"message_bytes": n, "framing": "600 (nonce||ct||tag, 25-byte header on the host)",
+           "device_seal_us": round(seal_us, 2), "device_open_us": round(open_us, 2),
+           "host_pinned_seal_open_us": round(host_us, 2), "verified": ok}
+    try:
+        C = ctypes.CDLL(os.path.join(ROOT, "tools", "libcpu_baseline.so"))
+        Pc, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        C.cb_aead_batch.argtypes = [I, I, Pc, Pc, Pc, S, Pc, S, I, ctypes.c_long, I]
+        pt = h_msg.numpy().copy()
+        ct = np.empty(n + 16, np.uint8)
+        bk = np.empty(n, np.uint8)
+        nn = np.frombuffer(bytes(range(12)), np.uint8).copy()
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 0.5:
+            C.cb_aead_batch(1, 0, KEY, nn.ctypes.data, pt.ctypes.data, n, ct.ctypes.data, n + 16, n, 1, 1)
+            assert C.cb_aead_batch(1, 1, KEY, nn.ctypes.data, ct.ctypes.data, n + 16, bk.ctypes.data, n, n, 1, 1) == 0
+            reps += 1
+        res["openssl_1core_seal_open_us"] = round((time.perf_counter() - t0) / reps * 1e6, 2)
+    except OSError as e:
+        res["openssl_1core_seal_open_us"] = {"error": str(e)}
+    ctx.close()
+    return res
+
+
 def cpu_baseline(workload: str, seconds: float = 10.0) -> dict:
     """Rank-0 CPU baselines on a bounded sample of the same workload shape.
     primary ('port'): the oracle's C restatement (oracle/liboracle.so), all host threads;
@@ -552,6 +640,10 @@ def main() -> None:
                 we.free()
             except Exception as e:  # report, never hide
                 extras[name] = {"error": repr(e)}
+        try:
+            extras["config1_message_64k"] = config1_message(local)
+        except Exception as e:
+            extras["config1_message_64k"] = {"error": repr(e)}
         try:
             extras["host_path_pcie"] = host_path_rate(local)
         except Exception as e:
