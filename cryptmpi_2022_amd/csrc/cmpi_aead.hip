@@ -221,7 +221,7 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   // weights are built from H on the host); records need >= 64 data blocks.
   const int fw = g_force_wide.load();
   const bool wide_ok = p.nb >= 64;
-  if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target && nx >= 1024))) {
+  if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target && nx >= 256))) {
     // A round = one wave per (record, chunk) on every CU (W waves); a wave's time ~ (fixed
     // staging/weight phases) + S steps.  Chunks are cut from the end with chunk 0 absorbing the
     // remainder (G <= its length < 2G), so 1 MiB records (nx = 2^16 + 1) split into exactly
@@ -231,7 +231,7 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     uint64_t S = g_force_S.load();
     if (!S) {
       double best = 1e300;
-      for (uint64_t s = std::min<uint64_t>(2, smax); s <= smax; s = c->dev_keys ? 2 * s : s + 1) {
+      for (uint64_t s = 1; s <= smax; s = c->dev_keys ? 2 * s : s + 1) {
         const uint64_t units = (uint64_t)nrec * std::max<uint64_t>(1, nx / (64 * s));
         const double est = (double)((units + W - 1) / W) * (double)(kWideFixedSteps + s);
         if (est < best) best = est, S = s;

@@ -45,7 +45,9 @@ for spec in args.libs:  # path[:sched] — the same .so may be loaded twice unde
 dev = torch.device("cuda:0")
 key = bytes(range(16))
 SHAPES = {"gcm1k": ("gcm", 65536, 1024), "gcm4k": ("gcm", 65536, 4096), "ocb1m": ("ocb", 4096, 1 << 20),
-          "ctr1g": ("ctr", 1, 1 << 30), "a2a": ("gcm", 8, 1 << 20), "a2a64": ("gcm", 64, 1 << 20)}
+          "ctr1g": ("ctr", 1, 1 << 30), "a2a": ("gcm", 8, 1 << 20), "a2a64": ("gcm", 64, 1 << 20),
+          "m4k": ("gcm", 1, 4096), "m64k": ("gcm", 1, 65536), "b8x4k": ("gcm", 8, 4096), "b256x4k": ("gcm", 256, 4096),
+          "m1m": ("gcm", 1, 1 << 20), "b1024x16k": ("gcm", 1024, 16384)}
 
 
 def ptr(t):
