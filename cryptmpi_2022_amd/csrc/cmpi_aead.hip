@@ -221,7 +221,8 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   // weights are built from H on the host); records need >= 64 data blocks.
   const int fw = g_force_wide.load();
   const bool wide_ok = p.nb >= 64;
-  if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target && nx >= 256))) {
+  if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target &&
+                                 (nx >= 256 || (uint64_t)nrec * p.L * nseg * 8 <= target)))) {
     // A round = one wave per (record, chunk) on every CU (W waves); a wave's time ~ (fixed
     // staging/weight phases) + S steps.  Chunks are cut from the end with chunk 0 absorbing the
     // remainder (G <= its length < 2G), so 1 MiB records (nx = 2^16 + 1) split into exactly
