@@ -50,6 +50,7 @@ _SIGS = {
     "cmpi_ctx_derive_subkey": ([_P, _P, _P], _P),
     "cmpi_ctx_rekey_subkey": ([_P, _P, _P, _P], _I),
     "cmpi_ctx_free": ([_P], None),
+    "cmpi_ctx_rekey": ([_P, _P, _S, _P], _I),
     "cmpi_ctx_device": ([_P], _I),
     "cmpi_host_register": ([_P, _S], _I),
     "cmpi_host_unregister": ([_P], _I),

@@ -49,21 +49,40 @@ def _open_checked(ctx, out, wire, n: int, p: int, what: str) -> None:
         raise N.CmpiError(N.CMPI_EAUTH, f"Decryption error: {what}")
 
 
+def _on_stream(stream):
+    """Run a whole collective on `stream` (None: the current stream): seal, transport and open
+    then share one stream, so the collective reads the wire only after the seal wrote it."""
+    import contextlib
+
+    import torch
+
+    return contextlib.nullcontext() if stream is None else torch.cuda.stream(stream)
+
+
+def _root_global(root: int, group) -> int:
+    """torch.distributed's src=/dst= take a GLOBAL rank; `root` is the rank within `group`
+    (the communicator's rank, as MPI's root argument)."""
+    import torch.distributed as dist
+
+    return root if group is None else dist.get_global_rank(group, root)
+
+
 def alltoall(ctx, sendbuf, recvbuf, n: int, group=None, stream=None) -> None:
     """MPIR_Naive_Sec_Alltoall: seal p blocks, all_to_all the ciphertext, open p blocks.
-    sendbuf/recvbuf: p*n bytes (device)."""
+    sendbuf/recvbuf: p*n bytes (device).  Everything runs on `stream` (default: current)."""
     import torch.distributed as dist
 
     p = dist.get_world_size(group)
-    wire, wire_in = _wire(p, n, sendbuf.device), _wire(p, n, sendbuf.device)
-    seal_blocks(ctx, wire, sendbuf, n, p, stream=stream)
-    if _host_transport(group):
-        h_in = wire_in.cpu()
-        dist.all_to_all_single(h_in, wire.cpu(), group=group)
-        wire_in.copy_(h_in)
-    else:
-        dist.all_to_all_single(wire_in, wire, group=group)
-    _open_checked(ctx, recvbuf, wire_in, n, p, "alltoall")
+    with _on_stream(stream):
+        wire, wire_in = _wire(p, n, sendbuf.device), _wire(p, n, sendbuf.device)
+        seal_blocks(ctx, wire, sendbuf, n, p)
+        if _host_transport(group):
+            h_in = wire_in.cpu()
+            dist.all_to_all_single(h_in, wire.cpu(), group=group)
+            wire_in.copy_(h_in)
+        else:
+            dist.all_to_all_single(wire_in, wire, group=group)
+        _open_checked(ctx, recvbuf, wire_in, n, p, "alltoall")
 
 
 def allgather(ctx, sendbuf, recvbuf, n: int, group=None) -> None:
@@ -96,13 +115,13 @@ def gather(ctx, sendbuf, recvbuf, n: int, root: int = 0, group=None) -> None:
     src = wire.cpu() if host else wire
     if rank == root:
         parts = [src.new_empty(n + BLOCK_OVERHEAD) for _ in range(p)]
-        dist.gather(src, parts, dst=root, group=group)
+        dist.gather(src, parts, dst=_root_global(root, group), group=group)
         wire_in = _wire(p, n, sendbuf.device)
         for i, t in enumerate(parts):
             wire_in[i * (n + BLOCK_OVERHEAD):(i + 1) * (n + BLOCK_OVERHEAD)].copy_(t)
         _open_checked(ctx, recvbuf, wire_in, n, p, "gather")
     else:
-        dist.gather(src, None, dst=root, group=group)
+        dist.gather(src, None, dst=_root_global(root, group), group=group)
 
 
 def scatter(ctx, sendbuf, recvbuf, n: int, root: int = 0, group=None) -> None:
@@ -120,9 +139,9 @@ def scatter(ctx, sendbuf, recvbuf, n: int, root: int = 0, group=None) -> None:
         seal_blocks(ctx, wire, sendbuf, n, p)
         src = wire.cpu() if host else wire
         parts = list(src.split(n + BLOCK_OVERHEAD))
-        dist.scatter(dst, parts, src=root, group=group)
+        dist.scatter(dst, parts, src=_root_global(root, group), group=group)
     else:
-        dist.scatter(dst, None, src=root, group=group)
+        dist.scatter(dst, None, src=_root_global(root, group), group=group)
     if host:
         mine.copy_(dst)
     _open_checked(ctx, recvbuf, mine, n, 1, "scatter")
@@ -139,7 +158,7 @@ def bcast(ctx, buf, n: int, root: int = 0, group=None) -> None:
         seal_blocks(ctx, wire, buf, n, 1)
     host = _host_transport(group)
     t = wire.cpu() if host else wire
-    dist.broadcast(t, src=root, group=group)
+    dist.broadcast(t, src=_root_global(root, group), group=group)
     if rank != root:
         if host:
             wire.copy_(t)

@@ -120,7 +120,7 @@ struct cmpi_ctx {
   int device = 0;
   int ncu = 256;
   uint8_t key[16];
-  bool dev_keys = false;  // key, rk, drk and H exist only on the device (derived 602 sub-key)
+  std::atomic<bool> dev_keys{false};  // key, rk, drk and H exist only on the device (derived 602 sub-key)
   cmpi::dev::RoundKeys nrk{};        // nonce DRBG key Kn (OS CSPRNG), cmpi_gcm_seal_batch_fresh
   std::atomic<uint64_t> nctr{0};     // nonce DRBG counter
   cmpi::dev::RoundKeys rk{};
@@ -132,9 +132,14 @@ struct cmpi_ctx {
   mutable std::map<uint32_t, std::array<Blk, 7>> mj;
   // wide-plan chunk weights H^(1 + (nch-1-i)·C) in HBM, per (C, nch) (host-keyed contexts)
   mutable std::map<std::pair<uint32_t, uint32_t>, void*> chw;
-  // internal scratch (partials, status) and staging for *_host
+  // internal scratch (partials, status) of device-resident calls that pass no workspace, and
+  // the event of its last user: the next user's stream waits on it, so NULL-workspace calls on
+  // one ctx from different streams are ordered (the host pipeline has scratch of its own)
   mutable void* scratch = nullptr;
   mutable size_t scratch_cap = 0;
+  mutable hipEvent_t scratch_ev = nullptr;
+  mutable bool scratch_used = false;
+  mutable std::mutex smu;  // scratch lease (held through the launches of one call)
   mutable uint8_t* stage = nullptr;
   mutable size_t stage_cap = 0;
   mutable hipStream_t hstream = nullptr;
@@ -162,6 +167,35 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
   *cap = sz;
   return CMPI_OK;
 }
+
+// Workspace of one batch call: the caller's buffer, or the context's scratch under a lease that
+// holds the ctx lock through the launches, makes the launch stream wait for the scratch's previous
+// user and records the new last use when it ends (NULL-workspace calls from two
+// streams used to overwrite each other's partials).
+struct ScratchLease {
+  const cmpi_ctx* c;
+  hipStream_t st;
+  std::unique_lock<std::mutex> lk;
+  uint8_t* ptr = nullptr;
+  bool internal = false;
+  ScratchLease(const cmpi_ctx* c_, void* workspace, hipStream_t st_) : c(c_), st(st_) {
+    ptr = (uint8_t*)workspace;
+  }
+  int acquire(size_t need) {
+    if (ptr || !need) return CMPI_OK;
+    lk = std::unique_lock<std::mutex>(c->smu);
+    internal = true;
+    if (!c->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
+    if (c->scratch_used) HIP_TRY(hipStreamWaitEvent(st, c->scratch_ev, 0));
+    int rc = ensure_buf(&c->scratch, &c->scratch_cap, need);
+    if (rc) return rc;
+    ptr = (uint8_t*)c->scratch;
+    return CMPI_OK;
+  }
+  ~ScratchLease() {
+    if (internal && hipEventRecord(c->scratch_ev, st) == hipSuccess) c->scratch_used = true;
+  }
+};
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device).
 std::mutex g_attr_mu;
@@ -306,12 +340,21 @@ int get_mj(const cmpi_ctx* c, uint32_t G, cmpi::dev::GcmCombineArgs& ca) {
 // j < 4 (the weights of chunk i's four quarter-wave sums, so the combine only XORs): built on
 // the host from H once per (C, nch) and kept in HBM for the context's lifetime.  Device-keyed
 // contexts (no host H) return null and keep the barrier-phased kernel + combine weighting.
-int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out) {
+// At most kChwCache entries per context (record lengths vary in the per-message regimes): a
+// full cache is dropped as a whole (hipFree orders itself after the work in flight).  The copy is
+// stream-ordered on the launch stream; the host vector is pageable, so hipMemcpyAsync has staged
+// it before returning.
+constexpr size_t kChwCache = 32;
+int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out, hipStream_t st) {
   *out = nullptr;
   if (c->dev_keys) return CMPI_OK;
   std::lock_guard<std::mutex> lk(c->mu);
   auto key = std::make_pair(C, nch);
   auto it = c->chw.find(key);
+  if (it == c->chw.end() && c->chw.size() >= kChwCache) {
+    for (auto& kv : c->chw) (void)hipFree(kv.second);
+    c->chw.clear();
+  }
   if (it == c->chw.end()) {
     std::vector<Blk> w((size_t)nch * 4);
     const Blk P = cmpi::gf_pow(c->H, C), H16 = cmpi::gf_pow(c->H, 16);
@@ -326,7 +369,7 @@ int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out) {
     }
     void* d = nullptr;
     if (hipMalloc(&d, (size_t)nch * 64) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc chunk weights failed");
-    if (hipMemcpy(d, w.data(), (size_t)nch * 64, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpyAsync(d, w.data(), (size_t)nch * 64, hipMemcpyHostToDevice, st) != hipSuccess) {
       (void)hipFree(d);
       return fail(CMPI_EHIP, "chunk weights copy failed");
     }
@@ -428,22 +471,19 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.nflag2_from = ns.flag2_from;
   memcpy(a.nfix, ns.fix, sizeof a.nfix);
   a.sched = (uint32_t)g_sched.load();
+  ScratchLease lease(c, workspace, st);
   if (p.wide) {
     if ((uint64_t)nrec * p.nseg * 16 > 0xFFFFFFFFull) return fail(CMPI_EINVAL, "too many chunks");
-    uint8_t* ws = (uint8_t*)workspace;
-    if (!ws) {
-      std::lock_guard<std::mutex> lk(c->mu);
-      int rc = ensure_buf(&c->scratch, &c->scratch_cap, gcm_ws_bytes(c, p, nrec));
-      if (rc) return rc;
-      ws = (uint8_t*)c->scratch;
-    }
+    int rc0 = lease.acquire(gcm_ws_bytes(c, p, nrec));
+    if (rc0) return rc0;
+    uint8_t* ws = lease.ptr;
     a.partial = reinterpret_cast<u32x4*>(ws);
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
     a.S = p.S;
     a.nch = p.nseg;
     int rc = get_h64tab(c, &a.htab);
     if (!rc) rc = get_wnib(c, &a.wtab);
-    if (!rc && g_wide_chw.load() && !(a.sched & 8u)) rc = get_chw(c, p.G, p.nseg, &a.chw);
+    if (!rc && g_wide_chw.load() && !(a.sched & 8u)) rc = get_chw(c, p.G, p.nseg, &a.chw, st);
     if (rc) return rc;
     a.probe = g_wide_probe.load();
     auto fn = a.chw ? cmpi::dev::gcm_wide_kernel<DEC, true> : cmpi::dev::gcm_wide_kernel<DEC, false>;
@@ -470,13 +510,9 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     return launch_gcm_combine<DEC>(c, ca, p.G, st);  // chunk i weighted by H^{(nch-1-i)·64S}, as segments
   }
   if (p.nseg > 1) {
-    uint8_t* ws = (uint8_t*)workspace;
-    if (!ws) {
-      std::lock_guard<std::mutex> lk(c->mu);
-      int rc = ensure_buf(&c->scratch, &c->scratch_cap, gcm_ws_bytes(c, p, nrec));
-      if (rc) return rc;
-      ws = (uint8_t*)c->scratch;
-    }
+    int rc0 = lease.acquire(gcm_ws_bytes(c, p, nrec));
+    if (rc0) return rc0;
+    uint8_t* ws = lease.ptr;
     a.partial = reinterpret_cast<u32x4*>(ws);
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
   }
@@ -546,13 +582,12 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const size_t part_bytes = (size_t)nrec * p.nchunks * 16;
   const size_t off_bytes = (size_t)nrec * 16;
   const size_t need = part_bytes + off_bytes + (size_t)nrec * 4;
-  uint8_t* ws = (uint8_t*)workspace;
-  if (!ws) {
-    std::lock_guard<std::mutex> lk(c->mu);
-    int rc = ensure_buf(&c->scratch, &c->scratch_cap, need);
-    if (rc) return rc;
-    ws = (uint8_t*)c->scratch;
+  ScratchLease lease(c, workspace, st);
+  {
+    int rc0 = lease.acquire(need);
+    if (rc0) return rc0;
   }
+  uint8_t* ws = lease.ptr;
   u32x4* d_part = reinterpret_cast<u32x4*>(ws);
   u32x4* d_off0 = reinterpret_cast<u32x4*>(ws + part_bytes);
   int32_t* st_arr = status ? status : reinterpret_cast<int32_t*>(ws + part_bytes + off_bytes);
@@ -724,8 +759,19 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   // every region and slot 2 MiB aligned (DMA into regions that straddle 2 MiB boundaries ran
   // 20.6 instead of 33 GiB/s in some allocation histories, tools/host_calls.py)
   auto up2m = [](size_t x) { return (x + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1); };
+  // kernel workspace of its own per slot (never the context's scratch, which device-resident
+  // calls on caller streams may hold): the larger of a full chunk's and the last chunk's
+  auto ws_for = [&](size_t nr) -> size_t {
+    if (!nr) return 0;
+    if (OCB) {
+      const OcbPlan op_ = plan_ocb(c, len, nr);
+      return (size_t)nr * op_.nchunks * 16 + nr * 16 + nr * 4;
+    }
+    return gcm_ws_bytes(c, plan_gcm(c, len, nr), nr);
+  };
+  const size_t ws_b = up16(std::max(ws_for(K), ws_for(nrec - (nrec - 1) / K * K)));
   const size_t in_b = up2m(ip * K), out_b = up2m(op * K), n_b = up16(npitch * K), st_b = up16(4 * K);
-  const size_t slot_b = up2m(in_b + out_b + n_b + st_b);
+  const size_t slot_b = up2m(in_b + out_b + n_b + st_b + ws_b);
   if (P.cap < slot_b) {
     for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
     if (P.buf) (void)hipFree(P.buf);
@@ -767,7 +813,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   };
   auto layout = [&](int sl, uint8_t* base) {
     struct L {
-      uint8_t *in, *out, *n;
+      uint8_t *in, *out, *n, *ws;
       int32_t* st;
     } l;
     if (base == P.buf) base = reinterpret_cast<uint8_t*>(up2m(reinterpret_cast<uintptr_t>(base)));
@@ -775,6 +821,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     l.out = l.in + in_b;
     l.n = l.out + out_b;
     l.st = reinterpret_cast<int32_t*>(l.n + n_b);
+    l.ws = l.n + n_b + st_b;
     return l;
   };
   // copy chunk ci's outputs from the pinned slot to the user's buffers (after its D2H)
@@ -814,10 +861,11 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     if ((rc = step("H2D", ci))) break;
     HIP_TRY(hipEventRecord(P.in_ready[sl], P.s[0]));
     HIP_TRY(hipStreamWaitEvent(P.s[1], P.in_ready[sl], 0));
+    void* wsp = ws_b ? (void*)d.ws : nullptr;
     if (OCB)
-      rc = ocb_batch<DEC>(c, d.out, op, d.in, ip, d.n, npitch, len, nr, DEC ? d.st : nullptr, nullptr, P.s[1]);
+      rc = ocb_batch<DEC>(c, d.out, op, d.in, ip, d.n, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
     else
-      rc = gcm_batch<DEC>(c, d.out, op, d.in, ip, d.n, npitch, len, nr, DEC ? d.st : nullptr, nullptr, P.s[1]);
+      rc = gcm_batch<DEC>(c, d.out, op, d.in, ip, d.n, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
     if (rc) break;
     if ((rc = step("kernel", ci))) break;
     HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
@@ -1020,10 +1068,15 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
 void cmpi_ctx_free(cmpi_ctx* c) {
   if (!c) return;
   DeviceGuard dg(c->device);
-  // Work of this context may still be in flight on any caller stream (stream-ordered batch
-  // calls, the key-setup kernel of a derived sub-key): drain the device before its tables,
-  // scratch and staging go back to the allocator.
-  (void)hipDeviceSynchronize();
+  // Drain the context's own streams and its scratch's last user (not the whole device: the
+  // per-message 602 path frees contexts at message rate).  Device-resident calls the caller
+  // enqueued on its own streams must be complete or ordered before the free, as for any buffer
+  // the caller releases (cmpi_aead.h); hipFree itself does not return memory still in use.
+  if (c->pipe && c->pipe->init)
+    for (auto& ps : c->pipe->s) (void)hipStreamSynchronize(ps);
+  if (c->hstream) (void)hipStreamSynchronize(c->hstream);
+  if (c->scratch_used) (void)hipEventSynchronize(c->scratch_ev);
+  if (c->scratch_ev) (void)hipEventDestroy(c->scratch_ev);
   if (c->scratch) (void)hipFree(c->scratch);
   for (auto& kv : c->chw) (void)hipFree(kv.second);
   if (c->stage) (void)hipFree(c->stage);
@@ -1301,7 +1354,19 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_keysetup_kernel), dst->device, cmpi::dev::kKsLds);
   if (rc) return rc;
   {
+    // The context's own streams (host pipeline, host-memory CTR/ECB) may still read the old
+    // tables: drain them first.  Work the caller enqueued on other streams of its own must be
+    // ordered before `stream` by the caller (cmpi_aead.h: derived contexts are stream-ordered).
+    std::lock_guard<std::mutex> hl(dst->hmu);
+    if (dst->pipe && dst->pipe->init)
+      for (auto& ps : dst->pipe->s) HIP_TRY(hipStreamSynchronize(ps));
+    if (dst->hstream) HIP_TRY(hipStreamSynchronize(dst->hstream));
+    if (dst->scratch_used) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, dst->scratch_ev, 0));
+  }
+  {
     std::lock_guard<std::mutex> lk(dst->mu);
+    for (auto& kv : dst->chw) (void)hipFree(kv.second);
+    dst->chw.clear();
     dst->mj.clear();
     dst->dev_keys = true;
     memset(dst->key, 0, 16);
@@ -1314,6 +1379,68 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   hipLaunchKernelGGL(cmpi::dev::gcm_tables_kernel, dim3((cmpi::dev::kTabEntries + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, ta);
   HIP_TRY(hipGetLastError());
+  return CMPI_OK;
+}
+
+// Re-key a context in place to a host-known key (no allocation, no host table build): the host
+// expands the key and computes H = E_K(0) (what the kernel arguments and the host-built weights
+// need), the key-setup kernel in mode 0 rebuilds every device table from K on `stream`.  The
+// drop-in's context pool (cmpi_evp_shim.cpp) turns CryptMPI's per-message EVP_AEAD_CTX_new
+// (send.c:588-599, recv.c:562-575) into this instead of an allocation + 450 KB upload.
+int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream) {
+  if (!c || !key) return fail(CMPI_EINVAL, "null argument");
+  if (key_len != 16) return fail(CMPI_EINVAL, "key_len must be 16 (AES-128)");
+  DeviceGuard dg(c->device);
+  cmpi::dev::KeysetupArgs a{};
+  memcpy(a.v, key, 16);
+  a.mode = 0;
+  a.te0 = c->dt->te0;
+  a.sqmat = reinterpret_cast<const u32x4*>(c->dt->sqmat[0]);
+  a.keys = c->dt->keys;
+  a.h2pow = reinterpret_cast<u32x4*>(c->dt->h2pow[0]);
+  a.chains = reinterpret_cast<u32x4*>(c->dt->chains[0]);
+  cmpi::dev::TablesArgs ta{};
+  ta.chains = a.chains;
+  ta.htab = reinterpret_cast<u32x4*>(c->dt->htab[0]);
+  ta.h64 = reinterpret_cast<u32x4*>(c->dt->h64);
+  ta.ntab = reinterpret_cast<u32x4*>(c->dt->ntab[0]);
+  ta.wnib = reinterpret_cast<u32x4*>(c->dt->wnib[0]);
+  int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_keysetup_kernel), c->device, cmpi::dev::kKsLds);
+  if (rc) return rc;
+  {
+    std::lock_guard<std::mutex> hl(c->hmu);
+    if (c->pipe && c->pipe->init)
+      for (auto& ps : c->pipe->s) HIP_TRY(hipStreamSynchronize(ps));
+    if (c->hstream) HIP_TRY(hipStreamSynchronize(c->hstream));
+    if (c->scratch_used) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, c->scratch_ev, 0));
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (auto& kv : c->chw) (void)hipFree(kv.second);
+  c->chw.clear();
+  c->mj.clear();
+  memcpy(c->key, key, 16);
+  cmpi::aes128_expand_words(key, c->rk.w);
+  cmpi::aes128_dec_words(c->rk.w, c->drk.w);
+  uint32_t z[4] = {0, 0, 0, 0}, h[4];
+  cmpi::aes128_encrypt_words_host(c->rk.w, z, h);
+  memcpy(c->H.b, h, 16);
+  c->dev_keys = false;
+  hipLaunchKernelGGL(cmpi::dev::gcm_keysetup_kernel, dim3(1), dim3(256), cmpi::dev::kKsLds, (hipStream_t)stream, a);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(cmpi::dev::gcm_tables_kernel, dim3((cmpi::dev::kTabEntries + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, ta);
+  HIP_TRY(hipGetLastError());
+  if (c->alg == CMPI_AES_128_OCB) {  // RFC 7253 L table from L_* = E_K(0) (host, 1 KiB)
+    uint8_t lt[66][16];
+    memcpy(lt[0], c->H.b, 16);
+    for (int i = 1; i < 66; ++i) {
+      const uint8_t carry = lt[i - 1][0] >> 7;
+      for (int j = 0; j < 15; ++j) lt[i][j] = (uint8_t)((lt[i - 1][j] << 1) | (lt[i - 1][j + 1] >> 7));
+      lt[i][15] = (uint8_t)((lt[i - 1][15] << 1) ^ (carry ? 0x87 : 0));
+    }
+    HIP_TRY(hipMemcpyAsync(c->dt->ltab, lt, sizeof lt, hipMemcpyHostToDevice, (hipStream_t)stream));
+  }
+  if (!stream) HIP_TRY(hipStreamSynchronize(nullptr));  // NULL stream: synchronous re-key
   return CMPI_OK;
 }
 

@@ -34,8 +34,12 @@
  * appended after the ciphertext.  open verifies in constant-time-free batch form: a record
  * whose tag mismatches gets status 0 and its plaintext output zero-filled (aead.h:276-278).
  * Contexts are immutable after creation and may be used concurrently from several threads /
- * streams (aead.h:240-241) as long as each concurrent call passes its own `workspace`
- * (or calls are serialised on one stream).  Nothing is retained after a call returns.
+ * streams (aead.h:240-241).  A call with workspace == NULL borrows the context's internal
+ * scratch: the library orders such calls (the launch stream waits for the scratch's previous
+ * user), so they serialise on the device; pass a `workspace` per stream to run concurrently.
+ * The *_host calls use staging and scratch of their own.  Nothing is retained after a call
+ * returns; device-resident work must be complete (or ordered before it) when the caller frees
+ * a context or its buffers.
  */
 #ifndef CMPI_AEAD_H
 #define CMPI_AEAD_H
@@ -84,6 +88,13 @@ cmpi_ctx *cmpi_ctx_new(int alg, const uint8_t *key, size_t key_len, size_t tag_l
 cmpi_ctx *cmpi_ctx_derive_subkey(const cmpi_ctx *base, const uint8_t v[16], void *stream);
 int cmpi_ctx_rekey_subkey(cmpi_ctx *dst, const cmpi_ctx *base, const uint8_t v[16], void *stream);
 cmpi_ctx *cmpi_ctx_new_subkey(const cmpi_ctx *base, const uint8_t v[16]);
+/* Re-key an existing context in place to a new host-known key (what a fresh cmpi_ctx_new would
+ * hold, without its allocation and table upload): the device tables are rebuilt by a key-setup
+ * kernel enqueued on `stream`; use the context on that stream or after synchronising it
+ * (stream NULL: returns when the tables are built).
+ * Replaces EVP_AEAD_CTX_new for the per-message 602 contexts (send.c:588-599, recv.c:562-575)
+ * in the drop-in's context pool. */
+int cmpi_ctx_rekey(cmpi_ctx *ctx, const uint8_t *key, size_t key_len, void *stream);
 void cmpi_ctx_free(cmpi_ctx *ctx);
 int cmpi_ctx_device(const cmpi_ctx *ctx);
 /* Pin (page-lock) a host buffer for DMA, e.g. MPI send/receive buffers reused across calls, so
@@ -102,8 +113,8 @@ int cmpi_host_unregister(void *ptr);
  * not overlap each other; out may equal in (in-place) but must not partially overlap it.
  * The naive-collective wire layout nonce(12)||ct(n)||tag(16) is expressed as
  *   out = wire + 12, nonces = wire, out_stride = nonce_stride = n + 28.
- * workspace: NULL (use the context's internal scratch; calls on one ctx then must be
- * stream-ordered) or a device buffer of cmpi_gcm_workspace_size(len, nrec) bytes. */
+ * workspace: NULL (the context's internal scratch; the library orders such calls across
+ * streams) or a device buffer of cmpi_gcm_workspace_size(len, nrec) bytes. */
 size_t cmpi_gcm_workspace_size(const cmpi_ctx *ctx, size_t len, size_t nrec);
 int cmpi_gcm_seal_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
                         size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,

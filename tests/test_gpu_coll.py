@@ -77,7 +77,7 @@ def test_bench_alltoall_e2e_one_rank(n):
     assert res["ranks"] == 1 and res["all_blocks_authenticated"] and res["ms_per_call"] > 0
 
 
-def _coll_rank(rank: int, ws: int, port: int, q):
+def _coll_rank(rank: int, ws: int, port: int, q, n: int = 3000):
     import os
     import traceback
 
@@ -86,16 +86,22 @@ def _coll_rank(rank: int, ws: int, port: int, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=ws)
-        torch.cuda.set_device(0)  # one GPU box: both ranks share cuda:0, ciphertext moves on the host
-        ctx = aead.AeadCtx(KEY)
-        n = 3000
+        # RCCL between GPUs when every rank has one; otherwise (one GPU box) every rank shares
+        # cuda:0 and the ciphertext moves over gloo through host memory
+        rccl = torch.cuda.device_count() >= ws
+        torch.cuda.set_device(rank if rccl else 0)
+        dist.init_process_group("nccl" if rccl else "gloo", rank=rank, world_size=ws)
+        ctx = aead.AeadCtx(KEY, device=torch.cuda.current_device())
         plain = lambda r, i: records(0xC011 + 16 * r + i, 1, n)[0]  # noqa: E731  block (rank r, index i)
         dv = lambda a: torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).cuda()  # noqa: E731
         res = {}
-        # alltoall: rank r sends block (r, i) to rank i
+        # alltoall: rank r sends block (r, i) to rank i — on a side stream (everything ordered on it)
         recv = torch.empty(ws * n, dtype=torch.uint8, device="cuda")
-        coll.alltoall(ctx, dv(np.stack([plain(rank, i) for i in range(ws)])), recv, n)
+        side = torch.cuda.Stream()
+        send = dv(np.stack([plain(rank, i) for i in range(ws)]))
+        side.wait_stream(torch.cuda.current_stream())
+        coll.alltoall(ctx, send, recv, n, stream=side)
+        torch.cuda.current_stream().wait_stream(side)
         res["alltoall"] = np.array_equal(recv.cpu().numpy().reshape(ws, n), np.stack([plain(r, rank) for r in range(ws)]))
         # allgather
         recv = torch.empty(ws * n, dtype=torch.uint8, device="cuda")
@@ -113,6 +119,21 @@ def _coll_rank(rank: int, ws: int, port: int, q):
         buf = dv(plain(1, 7)) if rank == 1 else torch.zeros(n, dtype=torch.uint8, device="cuda")
         coll.bcast(ctx, buf, n, root=1)
         res["bcast"] = np.array_equal(buf.cpu().numpy(), plain(1, 7))
+        if ws >= 3:
+            # a sub-communicator {1, 2}: root 0 of the group is global rank 1 (MPI semantics)
+            sub = dist.new_group([1, 2])
+            if rank in (1, 2):
+                g = rank - 1
+                recv = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+                coll.gather(ctx, dv(plain(rank, 3)), recv, n, root=0, group=sub)
+                res["sub_gather"] = g != 0 or np.array_equal(recv.cpu().numpy().reshape(2, n), np.stack([plain(1, 3), plain(2, 3)]))
+                recv = torch.empty(n, dtype=torch.uint8, device="cuda")
+                coll.scatter(ctx, dv(np.stack([plain(1, 4), plain(1, 5)])) if g == 0 else None, recv, n, root=0, group=sub)
+                res["sub_scatter"] = np.array_equal(recv.cpu().numpy(), plain(1, 4 + g))
+                buf = dv(plain(2, 6)) if g == 1 else torch.zeros(n, dtype=torch.uint8, device="cuda")
+                coll.bcast(ctx, buf, n, root=1, group=sub)
+                res["sub_bcast"] = np.array_equal(buf.cpu().numpy(), plain(2, 6))
+            dist.barrier()
         torch.cuda.synchronize()
         dist.destroy_process_group()
         q.put((rank, res))
@@ -120,10 +141,7 @@ def _coll_rank(rank: int, ws: int, port: int, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_naive_collectives_two_processes():
-    """The five naive secure collectives end to end across two processes (gloo host transport of
-    the wire blocks, one GPU shared by both ranks): every rank gets the reference semantics'
-    plaintext back, every block authenticated."""
+def _run_ranks(ws: int, n: int):
     import socket
 
     import torch.multiprocessing as mp
@@ -133,12 +151,27 @@ def test_naive_collectives_two_processes():
         port = s.getsockname()[1]
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
-    procs = [ctxm.Process(target=_coll_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctxm.Process(target=_coll_rank, args=(r, ws, port, q, n)) for r in range(ws)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=150) for _ in range(2))
+    out = dict(q.get(timeout=150) for _ in range(ws))
     for p in procs:
         p.join(timeout=60)
-    for r in range(2):
+    for r in range(ws):
         assert isinstance(out[r], dict), out[r]
         assert all(out[r].values()), (r, out[r])
+
+
+@pytest.mark.parametrize("n", [3000, 1 << 20])
+def test_naive_collectives_two_processes(n):
+    """The five naive secure collectives end to end across two processes (RCCL when each rank has
+    a GPU, else gloo host transport with one GPU shared by both ranks), 3000-byte and config-5
+    1 MiB blocks, alltoall on a non-current stream: every rank gets the reference semantics'
+    plaintext back, every block authenticated."""
+    _run_ranks(2, n)
+
+
+def test_naive_collectives_subgroup_three_processes():
+    """Three ranks; gather / scatter / bcast on the sub-communicator {1, 2} with group roots
+    (root 0 of the group = global rank 1)."""
+    _run_ranks(3, 4096)

@@ -77,3 +77,34 @@ def test_ctypes_seal_open_semantics():
     # AAD is not supported by the drop-in (CryptMPI never passes any)
     assert L.EVP_AEAD_CTX_seal(ctx, out, ctypes.byref(olen), 349, nonce, 12, pt, 333, b"ad", 2) == 0
     L.EVP_AEAD_CTX_free(ctx)
+
+
+@pytest.mark.parametrize("threads,msgs,n", [(8, 16, 4096), (8, 4, 65536), (3, 5, 1001), (8, 2, 0)])
+def test_c_client_threads_share_one_ctx(tmp_path, threads, msgs, n):
+    """An OpenMP-style team of pthreads sealing and opening on ONE shared EVP_AEAD_CTX through the
+    drop-in (coalesced into batch launches), bit-exact vs the oracle; per-message 602 contexts
+    (T x EVP_AEAD_CTX_new of a fresh key per message, pooled + re-keyed on the device); libcrypto's
+    EVP_aes_256_ecb forwarded by the shim, not misread."""
+    import json
+
+    exe = tmp_path / "evp_mt_client"
+    subprocess.check_call(["gcc", "-O1", "-o", str(exe), os.path.join(ROOT, "tests", "evp_mt_client.c"),
+                           f"-L{os.path.dirname(SHIM)}", "-lcmpi_evp", "-lcrypto", "-lpthread",
+                           f"-Wl,-rpath,{os.path.dirname(SHIM)}"])
+    R = threads * msgs
+    key = splitmix64_bytes(0xBB, 16).tobytes()
+    nonces = random_nonces(0xBC, R)
+    pt = splitmix64_bytes(0xBD, n * R)
+    inp, outp = tmp_path / "in.bin", tmp_path / "out.bin"
+    inp.write_bytes(key + nonces.tobytes() + pt.tobytes())
+    r = subprocess.run([str(exe), str(threads), str(msgs), str(n), str(inp), str(outp)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["forwarded_aes256_ok"] == 1
+    out = outp.read_bytes()
+    for i in range(R):
+        got = out[i * (n + 16):(i + 1) * (n + 16)]
+        assert got == oracle.gcm_seal(key, nonces[i].tobytes(), pt[i * n:(i + 1) * n].tobytes()), i
+    assert out[R * (n + 16):] == oracle.ecb_encrypt(key, bytes((7 * i) & 0xFF for i in range(16)))
+    print("evp_mt", json.dumps(rec))
