@@ -91,6 +91,22 @@ _SIGS = {
     "cmpi_600_header": ([_U32, ctypes.c_uint8, _P], _I),
     "cmpi_600_seal": ([_P, _P, _P, _P, _S, _P], _I),
     "cmpi_600_open": ([_P, _P, _P, _S, _P, _P], _I),
+    "cmpi_700_send": ([_P, _P, _P, _P, _S, _P, _P, _P], _I),
+    "cmpi_700_recv": ([_P, _P, _P, _P, _P, _P], _I),
+    "cmpi_702_sender_new": ([_P, _P, _S, _I, _P], _P),
+    "cmpi_702_sender_free": ([_P], None),
+    "cmpi_702_sender_state": ([_P, _P], _I),
+    "cmpi_702_send": ([_P, _I, _P, _S, _P, _P, _P], _I),
+    "cmpi_702_precompute": ([_P, _S, _I, _P], _I),
+    "cmpi_702_recv_premask": ([_P, _P, _P, _P, _S, _P, _P], _I),
+    "cmpi_702_recv": ([_P, _P, _P, _P, _P, _P, _S, _P], _I),
+    "cmpi_gcm_seal_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P], _I),
+    "cmpi_gcm_open_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
+    "cmpi_ocb_seal_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P], _I),
+    "cmpi_ocb_open_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
+    "cmpi_test": ([_P, _P], _I),
+    "cmpi_wait": ([_P], _I),
+    "cmpi_waitall": ([_P, _S], _I),
     "cmpi_debug_force_plan": ([_I, _U32], None),
     "cmpi_debug_force_wide": ([_I, _U32], None),
     "cmpi_debug_set_gcm_prefetch": ([_I], None),

@@ -153,6 +153,27 @@ class AeadCtx(_Ctx):
             N.check(rc)
         return out, status
 
+    # ------------------------------------------------------------ asynchronous host batches
+    def seal_host_begin(self, nonces: np.ndarray, pt: np.ndarray, out: np.ndarray) -> "Request":
+        """MPI_Isend-style: enqueue the seal of (N, n) host plaintexts into out (N, n+16) and
+        return a Request (include/cmpi_async.h); out must stay alive until it completes."""
+        nrec, n = pt.shape
+        pt, nonces = np.ascontiguousarray(pt), np.ascontiguousarray(nonces)
+        fn = N.lib().cmpi_gcm_seal_host_begin if self._gcm else N.lib().cmpi_ocb_seal_host_begin
+        r = ctypes.c_void_p()
+        N.check(fn(self._h, out.ctypes.data, out.strides[0], pt.ctypes.data, max(pt.strides[0], 1),
+                   nonces.ctypes.data, 12, n, nrec, ctypes.byref(r)))
+        return Request(r, keep=(out,))
+
+    def open_host_begin(self, nonces: np.ndarray, ct_tag: np.ndarray, out: np.ndarray, status: np.ndarray) -> "Request":
+        nrec, m = ct_tag.shape
+        ct_tag, nonces = np.ascontiguousarray(ct_tag), np.ascontiguousarray(nonces)
+        fn = N.lib().cmpi_gcm_open_host_begin if self._gcm else N.lib().cmpi_ocb_open_host_begin
+        r = ctypes.c_void_p()
+        N.check(fn(self._h, out.ctypes.data, max(out.strides[0], 1), ct_tag.ctypes.data, ct_tag.strides[0],
+                   nonces.ctypes.data, 12, m - TAG_LEN, nrec, status.ctypes.data, ctypes.byref(r)))
+        return Request(r, keep=(out, status))
+
     def seal(self, nonce: bytes, pt: bytes) -> bytes:
         """EVP_AEAD_CTX_seal for one message (host memory)."""
         if len(nonce) != NONCE_LEN:
@@ -166,6 +187,37 @@ class AeadCtx(_Ctx):
             return None
         out, st = self.open_host_batch(np.frombuffer(nonce, np.uint8)[None, :], np.frombuffer(ct_tag, np.uint8)[None, :])
         return out[0].tobytes() if st[0] == 1 else None
+
+
+class Request:
+    """An outstanding asynchronous host batch (cmpi_req): test() ~ MPI_Test, wait() ~ MPI_Wait.
+    wait() returns CMPI_OK or CMPI_EAUTH (open: some record failed) and raises on errors."""
+
+    def __init__(self, handle, keep=()):
+        self._r = handle
+        self._keep = keep
+
+    def test(self) -> bool:
+        if self._r is None:
+            return True
+        done = ctypes.c_int(0)
+        rc = N.lib().cmpi_test(self._r, ctypes.byref(done))
+        if done.value:
+            self._r = None
+            self._keep = ()
+            if rc not in (N.CMPI_OK, N.CMPI_EAUTH):
+                N.check(rc)
+        return bool(done.value)
+
+    def wait(self) -> int:
+        if self._r is None:
+            return N.CMPI_OK
+        rc = N.lib().cmpi_wait(self._r)
+        self._r = None
+        self._keep = ()
+        if rc not in (N.CMPI_OK, N.CMPI_EAUTH):
+            N.check(rc)
+        return rc
 
 
 class CipherCtx(_Ctx):

@@ -1478,3 +1478,5 @@ cmpi_ctx* cmpi_ctx_new_subkey(const cmpi_ctx* base, const uint8_t v[16]) {
 
 #include "frame_host.hpp"
 #include "ring_host.hpp"
+#include "ctrmode_host.hpp"
+#include "async_host.hpp"

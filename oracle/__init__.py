@@ -49,11 +49,18 @@ def lib() -> ctypes.CDLL:
             "orc_ocb_seal_batch": [P, P, S, P, S, P, S, S, S, I],
             "orc_nonce602": [P, ctypes.c_uint8, ctypes.c_uint32],
             "orc_header600": [P, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_uint32],
+            "orc_700_send": [P, P, P, P, I, P, P],
+            "orc_700_recv": [P, P, P, P, P],
+            "orc_702_init": [P, P, P, P, I, I],
+            "orc_702_send": [P, I, P, I, P, P],
+            "orc_702_precompute": [P, I, I],
+            "orc_702_recv": [P, P, P, P, P, I],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = ctypes.c_int if name in ("orc_gcm_seal", "orc_gcm_open", "orc_ocb_seal", "orc_ocb_open") else None
+            fn.restype = ctypes.c_int if name in ("orc_gcm_seal", "orc_gcm_open", "orc_ocb_seal", "orc_ocb_open",
+                                                  "orc_702_send", "orc_702_precompute", "orc_702_recv") else None
         _lib = L
     return _lib
 
@@ -234,3 +241,59 @@ def mask_decrypt(key: bytes, iv: bytes, counter: int, mask: bytes, data: bytes) 
     lib().orc_mask_decrypt(_buf(key), _buf(iv), ctypes.c_ulong(counter), _buf(mask) if mask else None, len(mask),
                            _buf(data) if data else None, len(data), out)
     return bytes(out)[: len(data)]
+
+
+# ---------------------------------------------------------------- counter-mode messages (700 / 702)
+def send700(key: bytes, send_iv: bytes, counter: int, pt: bytes):
+    """MPI_SEC_BaseCounter_Pipeline_Send (send.c:886-1017): (header[26], ct, next counter)."""
+    c = ctypes.c_ulong(counter)
+    hdr = (ctypes.c_uint8 * 26)()
+    out = (ctypes.c_uint8 * max(1, len(pt)))()
+    lib().orc_700_send(_buf(key), _buf(send_iv), ctypes.byref(c), _buf(pt) if pt else None, len(pt), hdr, out)
+    return bytes(hdr), bytes(out)[: len(pt)], c.value
+
+
+def recv700(key: bytes, recv_iv: bytes, hdr: bytes, ct: bytes) -> bytes:
+    out = (ctypes.c_uint8 * max(1, len(ct)))()
+    lib().orc_700_recv(_buf(key), _buf(recv_iv), _buf(hdr), _buf(ct) if ct else None, out)
+    return bytes(out)[: len(ct)]
+
+
+class _Sender702(ctypes.Structure):
+    _fields_ = [("ring", _Ring), ("ivb", ctypes.c_uint8 * 16), ("enc_common_counter_long_msg", ctypes.c_ulong),
+                ("counter_needto_send_large_msg", ctypes.c_ulong), ("series", ctypes.c_int)]
+
+
+class Sender702:
+    """One rank's 702 sender state (init.c:766-792 + send.c:1502-1987) over a ring of max_bytes."""
+
+    def __init__(self, key: bytes, send_iv: bytes, max_bytes: int = 8 << 20, series: int = 16):
+        self._mem = (ctypes.c_uint8 * max_bytes)()
+        self._s = _Sender702()
+        lib().orc_702_init(ctypes.byref(self._s), _buf(key), _buf(send_iv), self._mem, max_bytes, series)
+
+    def send(self, pt: bytes, pending: int = 0):
+        """-> (header[26], ciphertext)"""
+        hdr = (ctypes.c_uint8 * 26)()
+        out = (ctypes.c_uint8 * max(1, len(pt)))()
+        lib().orc_702_send(ctypes.byref(self._s), pending, _buf(pt) if pt else None, len(pt), hdr, out)
+        return bytes(hdr), bytes(out)[: len(pt)]
+
+    def precompute(self, n: int, rounds: int) -> int:
+        return lib().orc_702_precompute(ctypes.byref(self._s), n, rounds)
+
+    def state(self) -> dict:
+        s = self._s
+        r = s.ring
+        return {"start": r.start, "end": r.end, "compute_size": r.compute_size, "counter": r.counter,
+                "counter_needto_send": r.counter_needto_send,
+                "enc_common_counter_long_msg": s.enc_common_counter_long_msg,
+                "counter_needto_send_large_msg": s.counter_needto_send_large_msg}
+
+
+def recv702(key: bytes, recv_iv: bytes, hdr: bytes, ct: bytes, premask: bool = True) -> bytes:
+    """MPI_SEC_PreComputeCounter_Recv_v4 (recv.c:1025-1403); premask: mask generated while the
+    payload was in flight (recv.c:1107-1196), else the direct path."""
+    out = (ctypes.c_uint8 * max(1, len(ct)))()
+    lib().orc_702_recv(_buf(key), _buf(recv_iv), _buf(hdr), _buf(ct) if ct else None, out, 1 if premask else 0)
+    return bytes(out)[: len(ct)]

@@ -24,7 +24,7 @@ if [[ $WHAT == all || $WHAT == *smoke* ]]; then
   step smoke 240 "$out/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $WHAT == all || $WHAT == *test* ]]; then
-  step pytest_gpu 900 "$out/pytest_gpu.log" python -m pytest tests -m gpu -q -rf --timeout=300 ${PYTEST_K:+-k "$PYTEST_K"}
+  step pytest_gpu 900 "$out/pytest_gpu.log" python -u -m pytest tests -m gpu -q -rf --timeout 180 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 fi
 if [[ $WHAT == all || $WHAT == *bench* ]]; then
   step bench 600 "$out/bench.json" python bench.py ${BENCH_ARGS:-}
