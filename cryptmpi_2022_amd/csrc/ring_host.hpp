@@ -84,8 +84,9 @@ int cmpi_ctr_ring_state(const cmpi_ctr_ring* r, uint64_t st[5]) {
 // send.c:1162-1266
 int cmpi_ctr_ring_generate(cmpi_ctr_ring* r, size_t gen_bytes, void* stream) {
   if (!r) return fail(CMPI_EINVAL, "null ring");
-  // gen_bytes 0 is legal: like the reference it still makes one 16-byte block (send.c:1170)
-  if (gen_bytes > (size_t)r->max) return fail(CMPI_EINVAL, "gen_bytes out of range");
+  // gen_bytes 0 is legal: like the reference it still makes one 16-byte block (send.c:1170);
+  // more than the ring holds is refused by the head-room guard below (returns 0), as there
+  if (gen_bytes > 0x7FFFFFFFu) return fail(CMPI_EINVAL, "gen_bytes out of range");
   std::lock_guard<std::mutex> lk(r->mu);
   DeviceGuard dg(r->ctx->device);
   const int gen = (int)gen_bytes;
