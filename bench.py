@@ -541,6 +541,100 @@ def cpu_reference_baseline(workload: str, device: int) -> dict:
             "host": info, "round_trip": allr["round_trip"], "tags_match_gpu": match}
 
 
+def config1_exchange(n: int = 64 << 10, iters: int = 200) -> dict:
+    """BASELINE config 1's counterpart: 2-process secure MPI_Send/MPI_Recv ping-pong with 600
+    framing (tools/config1_exchange.py, child processes of this one), one-way latency per
+    message with GPU seal/open vs the same ping-pong in plaintext over the same transport."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "config1_exchange.py"), "--n", str(n),
+           "--iters", str(iters)]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
+                         env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    if out.returncode or not lines:
+        raise RuntimeError(f"config1_exchange rc={out.returncode}: {out.stderr.strip()[-400:]}")
+    return json.loads(lines[-1])
+
+
+def async_host_rate(device: int, n: int = 1 << 20, nreq: int = 64, reps: int = 3) -> dict:
+    """The isend/wait split on the host path (include/cmpi_async.h): nreq messages of n bytes
+    (pinned host buffers) sealed one after the other with the synchronous host call, vs all
+    begun at once (MPI_Isend eager encryption) and completed with waitall."""
+    from cryptmpi_2022_amd import _native as N
+
+    L = N.lib()
+    ctx = aead.AeadCtx(KEY, device=device)
+    pt = torch.randint(0, 256, (nreq, n), dtype=torch.uint8).pin_memory()
+    out = torch.empty((nreq, n + 16), dtype=torch.uint8).pin_memory()
+    nn = torch.randint(0, 256, (nreq, 12), dtype=torch.uint8).pin_memory()
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def sync():
+        for i in range(nreq):
+            N.check(L.cmpi_gcm_seal_host(ctx.handle, P(out[i]), n + 16, P(pt[i]), n, P(nn[i]), 12, n, 1))
+
+    def overlapped():
+        reqs = (ctypes.c_void_p * nreq)()
+        for i in range(nreq):
+            N.check(L.cmpi_gcm_seal_host_begin(ctx.handle, P(out[i]), n + 16, P(pt[i]), n, P(nn[i]), 12, n, 1,
+                                               ctypes.byref(reqs, i * ctypes.sizeof(ctypes.c_void_p))))
+        N.check(L.cmpi_waitall(reqs, nreq))
+
+    def rate(fn):
+        fn()
+        best = float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            best = min(best, time.perf_counter() - t0)
+        return nreq * n / best / GIB
+
+    r_sync, r_ovl = rate(sync), rate(overlapped)
+    ctx.close()
+    return {"config": f"{nreq} messages x {n} B GCM seal, pinned host buffers", "sync_host_GiBps": round(r_sync, 2),
+            "async_begin_waitall_GiBps": round(r_ovl, 2), "speedup": round(r_ovl / r_sync, 2)}
+
+
+def ctr702_rates(device: int, steps: int = 50) -> dict:
+    """702 messages device-resident (include/cmpi_ctrmode.h): 4 KiB from the mask ring (stream A,
+    one XOR pass) with the sender's precompute refilling it, 1 MiB and 8 MiB over stream B
+    (sliced CTR), receiver included; message rates from HIP events on the stream."""
+    from cryptmpi_2022_amd import ctrmode
+
+    ctx = aead.CipherCtx(KEY, "aes-128-ctr", device=device)
+    iv = bytes(range(32))
+    s = ctrmode.Sender702(ctx, iv)
+    res = {}
+    for n in (4096, 1 << 20, 8 << 20):
+        pt = torch.randint(0, 256, (n,), dtype=torch.uint8, device=f"cuda:{device}")
+        ct = torch.empty_like(pt)
+        back = torch.empty_like(pt)
+        mask = torch.empty(n + 1024, dtype=torch.uint8, device=f"cuda:{device}")
+        for _ in range(5):
+            hdr, _ = s.send(ct, pt, n)
+            s.precompute(n, 2)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            hdr, _ = s.send(ct, pt, n)
+            s.precompute(n, 2)
+            ml = ctrmode.recv702_premask(ctx, iv, hdr, mask)
+            ctrmode.recv702(ctx, iv, hdr, back, ct, mask=mask, mask_len=ml)
+        torch.cuda.synchronize(device)
+        dt = (time.perf_counter() - t0) / steps
+        res[f"{n}"] = {"us_per_message_send_precompute_recv": round(dt * 1e6, 2),
+                       "GiBps": round(n / dt / GIB, 2), "verified": bool(torch.equal(back, pt))}
+    s.close()
+    ctx.close()
+    return res
+
+
 def cpu_port_baseline(workload: str, seconds: float = 4.0) -> dict:
     """Secondary CPU datum: the oracle's C restatement (portable table AES, bit-serial GHASH;
     oracle/liboracle.so), all usable host threads, on a bounded sample of the workload."""
@@ -754,6 +848,12 @@ def main() -> None:
             extras["host_path_pcie"] = host_path_rate(local)
         except Exception as e:
             extras["host_path_pcie"] = {"error": repr(e)}
+        for name, fn in (("async_host", lambda: async_host_rate(local)), ("ctr702", lambda: ctr702_rates(local)),
+                         ("config1_exchange_64k", config1_exchange)):
+            try:
+                extras[name] = fn()
+            except Exception as e:  # report, never hide
+                extras[name] = {"error": repr(e)}
         result["extras"] = extras
     if not args.no_extras:  # config 5 end to end: a collective, so every rank runs it
         a2a = alltoall_e2e(local, pg, barrier)
