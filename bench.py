@@ -552,7 +552,7 @@ def config1_exchange(n: int = 64 << 10, iters: int = 200) -> dict:
         s_.bind(("127.0.0.1", 0))
         port = s_.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
-           "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "config1_exchange.py"), "--n", str(n),
+           "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "config1_exchange.py"), "--msg-bytes", str(n),
            "--iters", str(iters)]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
                          env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))

@@ -20,6 +20,7 @@ struct StagePool {
   std::mutex mu;
   std::multimap<size_t, void*> dev_free, host_free;
   std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> events;  // completion events of finished requests, reused
   size_t next = 0;
 };
 StagePool& stage_pool(int device) {
@@ -100,7 +101,10 @@ void req_release(cmpi_req* r) {
   StagePool& P = stage_pool(r->device);
   pool_give(P, false, r->dbuf, r->dcap);
   pool_give(P, true, r->hbuf, r->hcap);
-  if (r->done) (void)hipEventDestroy(r->done);
+  if (r->done) {
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.events.push_back(r->done);
+  }
   delete r;
 }
 
@@ -130,7 +134,15 @@ int host_begin(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t
   };
   int rc = pool_stream(P, &r->st);
   if (rc) return bail(rc);
-  if (hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return bail(fail(CMPI_EHIP, "event create failed"));
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (!P.events.empty()) {
+      r->done = P.events.back();
+      P.events.pop_back();
+    }
+  }
+  if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(CMPI_EHIP, "event create failed"));
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const bool in_pinned = in_rec && is_pinned(in), out_pinned = out_rec && is_pinned(out);
   const bool in_flat = in_pinned && (nrec == 1 || in_stride <= in_rec + 64);
@@ -164,12 +176,19 @@ int host_begin(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t
     } else if (in_rec) {
       HIP_TRY(hipMemcpyAsync(D + d_in, in, (nrec - 1) * ip + in_rec, hipMemcpyHostToDevice, st));
     }
-    for (size_t i = 0; i < nrec; ++i) memcpy(H + h_n + 16 * i, nonces + i * nonce_stride, 12);
-    HIP_TRY(hipMemcpyAsync(D + d_n, H + h_n, 16 * nrec, hipMemcpyHostToDevice, st));
     int32_t* dst = DEC ? (int32_t*)(D + d_st) : nullptr;
     void* wsp = ws ? (void*)(D + d_ws) : nullptr;
-    rc = OCB ? ocb_batch<DEC>(c, D + d_out, op, D + d_in, ip, D + d_n, 16, len, nrec, dst, wsp, st)
-             : gcm_batch<DEC>(c, D + d_out, op, D + d_in, ip, D + d_n, 16, len, nrec, dst, wsp, st);
+    if (!OCB && nrec == 1) {  // one message (an MPI_Isend): the nonce travels in the kernel arguments
+      NonceSpec ns;
+      ns.mode = 3;
+      memcpy(ns.fix, nonces, 12);
+      rc = gcm_batch<DEC>(c, D + d_out, op, D + d_in, ip, nullptr, 12, len, 1, dst, wsp, st, ns);
+    } else {
+      for (size_t i = 0; i < nrec; ++i) memcpy(H + h_n + 16 * i, nonces + i * nonce_stride, 12);
+      HIP_TRY(hipMemcpyAsync(D + d_n, H + h_n, 16 * nrec, hipMemcpyHostToDevice, st));
+      rc = OCB ? ocb_batch<DEC>(c, D + d_out, op, D + d_in, ip, D + d_n, 16, len, nrec, dst, wsp, st)
+               : gcm_batch<DEC>(c, D + d_out, op, D + d_in, ip, D + d_n, 16, len, nrec, dst, wsp, st);
+    }
     if (rc) return bail(rc);
     if (out_rec) {
       if (unpack)

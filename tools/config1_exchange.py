@@ -5,7 +5,7 @@ ping-pong in plaintext over the same transport (what the reference's config 1 me
 §0.3, 401 never encrypts).
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
-        --master-port 29555 tools/config1_exchange.py [--n 65536] [--iters 200]
+        --master-port 29555 tools/config1_exchange.py [--msg-bytes 65536] [--iters 200]
 
 Rank 0 prints one JSON line: one-way latency per message (round trip / 2), secure and plaintext.
 """
@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=64 << 10)
+    ap.add_argument("--msg-bytes", type=int, default=64 << 10)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     args = ap.parse_args()
@@ -40,8 +40,8 @@ def main() -> None:
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
     ctx = aead.AeadCtx(bytes(range(16)), device=dev)
-    ep = p2p.Endpoint(ctx, max_bytes=args.n)
-    msg = splitmix64_bytes(0xC1 + rank, args.n)
+    ep = p2p.Endpoint(ctx, max_bytes=args.msg_bytes)
+    msg = splitmix64_bytes(0xC1 + rank, args.msg_bytes)
     peer = 1 - rank
 
     def secure_round():
@@ -81,7 +81,7 @@ def main() -> None:
     dist.barrier()
     t_pl = (time.perf_counter() - t0) / args.iters / 2
     if rank == 0:
-        print(json.dumps({"message_bytes": args.n, "ranks": 2, "transport": "gloo (host memory)",
+        print(json.dumps({"message_bytes": args.msg_bytes, "ranks": 2, "transport": "gloo (host memory)",
                           "gpus": min(ngpu, 2), "framing": "600: header(25) + nonce||ct||tag",
                           "secure_one_way_us": round(t_sec * 1e6, 2), "plaintext_one_way_us": round(t_pl * 1e6, 2),
                           "crypto_added_us": round((t_sec - t_pl) * 1e6, 2), "round_trips_verified": ok}))
