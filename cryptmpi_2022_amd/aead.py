@@ -97,6 +97,12 @@ class AeadCtx(_Ctx):
             raise N.CmpiError(N.CMPI_EINVAL, N.last_error())
         return cls(b"", "aes-128-gcm", _handle=h)
 
+    def rekey(self, key: bytes, stream=None) -> None:
+        """Re-key this context in place to the host key `key` (cmpi_ctx_rekey: tables rebuilt on
+        the device, on `stream`; the drop-in's EVP_AEAD_CTX_new path)."""
+        kb = (ctypes.c_uint8 * len(key)).from_buffer_copy(bytes(key))
+        N.check(N.lib().cmpi_ctx_rekey(self._h, kb, len(key), _stream_ptr(stream)))
+
     def rekey_subkey(self, base: "_Ctx", v: bytes, stream=None) -> None:
         """Re-key this GCM context in place to K' = AES_K(V) on `stream` (no allocation)."""
         vb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(v))
@@ -262,6 +268,12 @@ def set_wide_chw(on: bool = True) -> None:
     """Test hook: wide GCM plan applies the chunk weights in the wide kernel (True, default) or in
     the combine kernel (False)."""
     N.lib().cmpi_debug_set_wide_chw(1 if on else 0)
+
+
+def set_flow(threads: int = 1024, flags: int = 0) -> None:
+    """Test hook (cmpi_debug.h cmpi_debug_set_flow): FLOW wide-kernel workgroup size and form
+    flags (bit 0 fused combine, bit 4 round-2 first form, bit 5 no automatic 512 threads)."""
+    N.lib().cmpi_debug_set_flow(threads, flags)
 
 
 def gcm_plan(ctx: AeadCtx, length: int, nrec: int):

@@ -86,9 +86,10 @@ struct DevTables {
   // device-keyed (602 sub-key) contexts: written by gcm_keysetup_kernel / gcm_tables_kernel
   uint8_t sqmat[31][128][16];    // columns of X -> X^(2^i), i = 1..31 (key independent, host)
   uint8_t h2pow[32][16];         // H^(2^i)
-  uint8_t chains[8][128][16];    // basis chains of H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
+  uint8_t chains[10][128][16];   // basis chains of H, H^2, H^3, H^4, H^8, H^16, H^32, H^64, H^12, H^48
   uint8_t h64[kByteTab];         // byte table of H^64 (wide plan)
   uint8_t wnib[7][kNibTab];      // nibble tables of H^(2^b), b < 7 (wide plan)
+  uint8_t fnib[10][kNibTab];     // nibble tables of H^1,2,3,4,8,12,16,32,48,64 (gcm_flow_kernel)
 };
 
 // Columns of the squaring maps X -> X^(2^i) (key setup of device-derived keys), once per process.
@@ -140,6 +141,9 @@ struct cmpi_ctx {
   mutable hipEvent_t scratch_ev = nullptr;
   mutable bool scratch_used = false;
   mutable std::mutex smu;  // scratch lease (held through the launches of one call)
+  // arrival counters of the FLOW wide kernel's fused combine (zero between launches; ordered
+  // like the scratch: the same lease)
+  mutable uint32_t* wcnt = nullptr;
   mutable uint8_t* stage = nullptr;
   mutable size_t stage_cap = 0;
   mutable hipStream_t hstream = nullptr;
@@ -168,6 +172,7 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
   return CMPI_OK;
 }
 
+constexpr uint32_t kWideCounters = 16384;  // records of one fused-combine wide launch, at most
 // Workspace of one batch call: the caller's buffer, or the context's scratch under a lease that
 // holds the ctx lock through the launches, makes the launch stream wait for the scratch's previous
 // user and records the new last use when it ends (NULL-workspace calls from two
@@ -181,15 +186,33 @@ struct ScratchLease {
   ScratchLease(const cmpi_ctx* c_, void* workspace, hipStream_t st_) : c(c_), st(st_) {
     ptr = (uint8_t*)workspace;
   }
-  int acquire(size_t need) {
-    if (ptr || !need) return CMPI_OK;
+  // order this call after the previous user of the context's scratch / counters
+  int order() {
+    if (internal) return CMPI_OK;
     lk = std::unique_lock<std::mutex>(c->smu);
     internal = true;
     if (!c->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
     if (c->scratch_used) HIP_TRY(hipStreamWaitEvent(st, c->scratch_ev, 0));
-    int rc = ensure_buf(&c->scratch, &c->scratch_cap, need);
+    return CMPI_OK;
+  }
+  int acquire(size_t need) {
+    if (ptr || !need) return CMPI_OK;
+    int rc = order();
+    if (rc) return rc;
+    rc = ensure_buf(&c->scratch, &c->scratch_cap, need);
     if (rc) return rc;
     ptr = (uint8_t*)c->scratch;
+    return CMPI_OK;
+  }
+  // the context's zeroed arrival counters (kWideCounters of them), allocated on first use
+  int counters(uint32_t** out) {
+    int rc = order();
+    if (rc) return rc;
+    if (!c->wcnt) {
+      HIP_TRY(hipMalloc(&c->wcnt, kWideCounters * 8 * sizeof(uint32_t)));  // per record: count, pad, 16-B accumulator
+      HIP_TRY(hipMemsetAsync(c->wcnt, 0, kWideCounters * 8 * sizeof(uint32_t), st));
+    }
+    *out = c->wcnt;
     return CMPI_OK;
   }
   ~ScratchLease() {
@@ -218,6 +241,7 @@ struct GcmPlan {
   uint32_t nb, nseg, G, r0;
   bool wide = false;  // gcm_wide_kernel: nseg = chunks per record, G = 64*S X-blocks per chunk
   uint32_t S = 0;
+  uint32_t nt = 0;    // FLOW kernel threads per workgroup (0: g_flow_nt)
 };
 
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
@@ -226,6 +250,8 @@ std::atomic<uint32_t> g_force_nseg{0};
 std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4/6
 std::atomic<int> g_wide_chw{1};       // wide plan, host-keyed: barrier-free FLOW kernel with chunk weights (1) or weights in the combine (0)
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
+std::atomic<int> g_flow_nt{1024};     // FLOW wide kernel threads per workgroup (512 / 1024), 0 = round-1 kernel
+std::atomic<int> g_flow_fused{0};     // FLOW wide kernel flags: bit 0 combine fused, bits 1-3 timing ablations, bit 4 round-2-first form, bit 5 no automatic 512-thread workgroups
 std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
 std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics: wide-kernel phase timestamps
@@ -261,7 +287,10 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     // staging/weight phases) + S steps.  Chunks are cut from the end with chunk 0 absorbing the
     // remainder (G <= its length < 2G), so 1 MiB records (nx = 2^16 + 1) split into exactly
     // 2^16 / G chunks instead of one extra 1-block chunk that would start a second round.
-    const uint64_t W = (uint64_t)c->ncu * (kGcmThreads / 64);
+    // FLOW (host-keyed): 512-thread workgroups, one per CU (228 VGPRs, no spills; 8 x 1 MiB at S = 4:
+    // 22.6 us vs 30.9 at 1024 threads, tools/ab_flow.py); round-1 kernel: 1024 threads
+    const bool flow = !c->dev_keys && g_wide_chw.load() && g_flow_nt.load();
+    const uint64_t W = (uint64_t)c->ncu * (flow ? 8 : kGcmThreads / 64);
     const uint64_t smax = std::max<uint64_t>(1, nx / 64);
     uint64_t S = g_force_S.load();
     if (!S) {
@@ -281,6 +310,10 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     p.G = (uint32_t)(64 * S);
     p.nseg = (uint32_t)std::max<uint64_t>(1, nx / p.G);
     p.r0 = (uint32_t)(nx - (uint64_t)(p.nseg - 1) * p.G);
+    // few waves (single messages, the 600/EVP regime; the naive alltoall's 8 x 1 MiB): 512-thread
+    // workgroups (1 x 64 KiB seal 21.0 -> 15.7 us at S = 2, tools/ab_flow.py)
+    if (g_flow_nt.load() == 1024 && !(g_flow_fused.load() & 32) && (uint64_t)nrec * p.nseg <= (uint64_t)c->ncu * 8)
+      p.nt = 512;
     return p;
   }
   uint64_t G = (nx + nseg - 1) / nseg;
@@ -295,7 +328,7 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
 
 // workspace: partials [nrec][nseg], E_K(J0) [nrec], and for device-keyed contexts H^{kG} [nseg]
 size_t gcm_ws_bytes(const cmpi_ctx* c, const GcmPlan& p, size_t nrec) {
-  if (p.wide) return (size_t)nrec * p.nseg * 16 + nrec * 16;
+  if (p.wide) return (size_t)nrec * p.nseg * 16 + nrec * 16;  // (E_K(J0) slots double as statuses)
   if (p.nseg <= 1) return 0;
   return (size_t)nrec * p.nseg * 16 + nrec * 16;
 }
@@ -381,6 +414,12 @@ int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out, hipS
 
 template <bool DEC>
 int launch_gcm_combine(const cmpi_ctx* c, cmpi::dev::GcmCombineArgs& ca, uint32_t G, hipStream_t st) {
+  if (ca.prew && !ca.ekj0) {  // partials already weighted, E_K(J0) inside: XOR only
+    hipLaunchKernelGGL(cmpi::dev::gcm_xor_combine_kernel<DEC>, dim3(ca.nrec), dim3(cmpi::dev::kXorCombineThreads), 128,
+                       st, ca);
+    HIP_TRY(hipGetLastError());
+    return CMPI_OK;
+  }
   int rc = get_mj(c, G, ca);
   if (rc) return rc;
   const uint32_t wpb = cmpi::dev::kCombineThreads / 64u;
@@ -486,14 +525,50 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     if (!rc && g_wide_chw.load() && !(a.sched & 8u)) rc = get_chw(c, p.G, p.nseg, &a.chw, st);
     if (rc) return rc;
     a.probe = g_wide_probe.load();
-    auto fn = a.chw ? cmpi::dev::gcm_wide_kernel<DEC, true> : cmpi::dev::gcm_wide_kernel<DEC, false>;
-    const size_t lds = a.chw ? (size_t)cmpi::dev::kGcmNib + 4 * 8192 : 2 * 65536;
-    if ((rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds))) return rc;
     const uint64_t waves = (uint64_t)nrec * p.nseg;
-    const uint32_t grid = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>((waves + kGcmThreads / 64 - 1) / (kGcmThreads / 64), (uint64_t)c->ncu));
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
-    HIP_TRY(hipGetLastError());
+    if (a.chw && g_flow_nt.load()) {
+      // FLOW kernel: NT threads per workgroup; radix-4 form unless disabled (flags bit 4);
+      // combine fused (counters + accumulators in the context's zeroed scratch) unless disabled
+      const int NT = p.nt ? (int)p.nt : g_flow_nt.load();
+      const int flags = g_flow_fused.load();
+      const bool r4 = !(flags & 16);
+      const bool fused = (flags & 1) && nrec <= kWideCounters;
+      if (fused) {
+        if ((rc = lease.counters(&a.wcnt))) return rc;
+        if (DEC && !status) {  // the verdicts go somewhere: the tail of the partials buffer
+          a.status = reinterpret_cast<int32_t*>(ws + (size_t)nrec * p.nseg * 16);
+        }
+      }
+      a.sched |= (uint32_t)((flags >> 1) & 7) << 8;  // timing ablations (cmpi_debug_set_flow)
+      a.wtab = r4 ? reinterpret_cast<const u32x4*>(c->dt->fnib[0]) : a.wtab;
+      const void* fn;
+      if (r4) fn = NT == 512 ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, true>)
+                             : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, true>);
+      else fn = NT == 512 ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, false>)
+                          : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, false>);
+      const size_t lds = r4 ? (size_t)cmpi::dev::kFlowLdsR4 : (size_t)cmpi::dev::kGcmNib + 4 * 8192;
+      if ((rc = set_lds_attr(fn, c->device, lds))) return rc;
+      const uint32_t wpb = (uint32_t)NT / 64u;
+      const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + wpb - 1) / wpb, (uint64_t)c->ncu));
+      void* kargs[] = {&a};
+      HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(NT), kargs, lds, st));
+      if (fused) {
+        if (DEC) {  // zero-fill failed records after the launch (gcm_flow_kernel: cross-XCD L2s)
+          hipLaunchKernelGGL(cmpi::dev::zero_failed_kernel, dim3((uint32_t)nrec), dim3(256), 0, st, out,
+                             (uint64_t)out_stride, (uint32_t)len, (const int32_t*)a.status);
+          HIP_TRY(hipGetLastError());
+        }
+        return CMPI_OK;
+      }
+    } else {
+      auto fn = a.chw ? cmpi::dev::gcm_wide_kernel<DEC, true> : cmpi::dev::gcm_wide_kernel<DEC, false>;
+      const size_t lds = a.chw ? (size_t)cmpi::dev::kGcmNib + 4 * 8192 : 2 * 65536;
+      if ((rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds))) return rc;
+      const uint32_t grid = (uint32_t)std::max<uint64_t>(
+          1, std::min<uint64_t>((waves + kGcmThreads / 64 - 1) / (kGcmThreads / 64), (uint64_t)c->ncu));
+      hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
+      HIP_TRY(hipGetLastError());
+    }
     cmpi::dev::GcmCombineArgs ca{};
     ca.in = in;
     ca.out = out;
@@ -1037,6 +1112,8 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
       if (b == 6) cmpi::build_byte_table(p, reinterpret_cast<Blk*>(ht->h64));  // p = H^64
       p = cmpi::gf_mul(p, p);
     }
+    for (uint32_t f = 0; f < cmpi::dev::kFlowNib; ++f)
+      cmpi::build_nibble_table(cmpi::gf_pow(c->H, cmpi::dev::flow_nib_exp(f)), reinterpret_cast<Blk*>(ht->fnib[f]));
   }
   if (alg == CMPI_AES_128_OCB) {
     // RFC 7253 §4.1: L_* = E_K(0), L_$ = double(L_*), L_0 = double(L_$), L_i = double(L_{i-1})
@@ -1078,6 +1155,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   if (c->scratch_used) (void)hipEventSynchronize(c->scratch_ev);
   if (c->scratch_ev) (void)hipEventDestroy(c->scratch_ev);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->wcnt) (void)hipFree(c->wcnt);
   for (auto& kv : c->chw) (void)hipFree(kv.second);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
@@ -1128,6 +1206,10 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
 }
 
 void cmpi_debug_set_wide_chw(int on) { g_wide_chw.store(on ? 1 : 0); }
+void cmpi_debug_set_flow(int threads, int fused) {
+  g_flow_nt.store(threads == 512 || threads == 1024 ? threads : (threads == 0 ? 0 : 1024));
+  g_flow_fused.store(fused);  // bit 0 fused combine; bits 1-3 timing ablations (wrong output); bit 4 !R4
+}
 
 // Timing events without the system-scope release fence (hipEventDisableSystemFence): a default
 // event's fence writes back and invalidates the caches and leaves a ~6 us bubble before the
@@ -1351,6 +1433,7 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   ta.h64 = reinterpret_cast<u32x4*>(dst->dt->h64);
   ta.ntab = reinterpret_cast<u32x4*>(dst->dt->ntab[0]);
   ta.wnib = reinterpret_cast<u32x4*>(dst->dt->wnib[0]);
+  ta.fnib = reinterpret_cast<u32x4*>(dst->dt->fnib[0]);
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_keysetup_kernel), dst->device, cmpi::dev::kKsLds);
   if (rc) return rc;
   {
@@ -1405,6 +1488,7 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
   ta.h64 = reinterpret_cast<u32x4*>(c->dt->h64);
   ta.ntab = reinterpret_cast<u32x4*>(c->dt->ntab[0]);
   ta.wnib = reinterpret_cast<u32x4*>(c->dt->wnib[0]);
+  ta.fnib = reinterpret_cast<u32x4*>(c->dt->fnib[0]);
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_keysetup_kernel), c->device, cmpi::dev::kKsLds);
   if (rc) return rc;
   {

@@ -61,6 +61,9 @@ struct GcmArgs {
   // for the four quarter-wave sums of chunk i (chunk 0 adds E_K(J0): the combine only XORs)
   const u32x4* chw;
   uint64_t* probe;  // diagnostics (cmpi_debug_set_wide_probe): per-WG phase timestamps, or null
+  // FLOW kernel, fused combine: per-record arrival counters (context memory, zero between
+  // launches) and, for open, the received tags / status; null = partials for gcm_combine_kernel
+  uint32_t* wcnt;
   RoundKeys rk;
 };
 
@@ -477,6 +480,314 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- FLOW wide kernel
+// The host-keyed wide decomposition as its own kernel (gcm_wide_kernel<.., FLOW> below is the
+// round-1 form, kept for the A/B knob): NT threads per workgroup (512 or 1024), every table load
+// issued before any LDS store (one global round trip for the tables).  Two forms:
+//  - R4 (default): the chunk's X blocks are folded per lane by Horner in H^64 (nibble table),
+//    the 64 lane accumulators by a radix-4 tree — three levels, each ONE nibble multiply per
+//    active lane by a lane-chosen table (H^1..3, H^4..12, H^16..48), lanes packed low so a level
+//    touches 3, 1, 1 LDS lane groups — and the chunk weight H^(1 + (nch-1-i)C) by one
+//    wave-cooperative product (gmul_wave).  Tables: 10 nibble tables (80 KiB) + AES rows.
+//  - !R4 (round-2 first form): Horner in H^64 by its byte table (64 KiB), a 4-level radix-2 tree,
+//    four products by the host weights M_j (gmul_wave4).
+// Combine fused in (a.wcnt != null): R4 XORs its workgroup's partials per record in LDS and one
+// lane per record XORs them into the record's accumulator (two 8-B agent atomics), waits, and
+// adds the number of chunks to the record's counter; the adder that completes the count loads
+// the accumulator (8-B agent atomic loads) and writes the tag / verdict, then zeroes both for
+// the next launch — MI355X_MICROARCH.md "Valid forms" ({8-B agent atomics both sides}, row 1:
+// one lane per storing workgroup, the last adder told by its add's return).  !R4 publishes each
+// wave's partial write-through and counts per wave (one add per chunk: contended).
+constexpr uint32_t kFlowAgg = 147456u;         // R4: aggregation slots, 16 x 16 B partials + 16 x 4 B records
+constexpr uint32_t kFlowLdsR4 = kFlowAgg + 512u;
+__device__ __forceinline__ uint32_t flow_tab(uint32_t f) {  // R4 nibble table f (keysetup_kernels.hpp flow_nib_exp)
+  return f < 8u ? f * 8192u : 131072u + (f - 8u) * 8192u;
+}
+
+template <int NT, bool R4>
+__device__ __forceinline__ void stage_flow(const GcmArgs& a) {
+  constexpr int kR = 1024 / NT, kH = R4 ? 0 : 4096 / NT, kW = (R4 ? 5120 : 2048) / NT;  // loads per thread
+  uint32_t rv[kR];
+  u32x4 hv[kH > 0 ? kH : 1], wv[kW];
+  const uint32_t t = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < kR; ++j) rv[j] = a.te0[(t + j * NT) >> 2];
+#pragma unroll
+  for (int j = 0; j < kH; ++j) hv[j] = a.htab[t + j * NT];
+#pragma unroll
+  for (int j = 0; j < kW; ++j) wv[j] = a.wtab[t + j * NT];
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {  // row image: entry e -> 64 words (Te0 x32 | Te1 x32), 4 threads
+    const uint32_t i = t + j * NT, e = i >> 2, q = i & 3u;
+    const uint32_t v = q >= 2u ? rotl8(rv[j]) : rv[j];
+    const u32x4 w = {v, v, v, v};
+    const uint32_t o = kGcmRows + e * 256u + q * 64u;
+    lds_st128(o, w);
+    lds_st128(o + 16u, w);
+    lds_st128(o + 32u, w);
+    lds_st128(o + 48u, w);
+  }
+#pragma unroll
+  for (int j = 0; j < kH; ++j) lds_st128((t + j * NT) * 16u, hv[j]);
+#pragma unroll
+  for (int j = 0; j < kW; ++j) {
+    const uint32_t e = t + j * NT;
+    lds_st128(R4 ? flow_tab(e >> 9) + (e & 511u) * 16u : kGcmNib + e * 16u, wv[j]);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ u32x4 shfl4(u32x4 v, uint32_t src) {
+  u32x4 r;
+  r[0] = __shfl((int)v[0], (int)src);
+  r[1] = __shfl((int)v[1], (int)src);
+  r[2] = __shfl((int)v[2], (int)src);
+  r[3] = __shfl((int)v[3], (int)src);
+  return r;
+}
+
+// Radix-4 lane tree: returns (lane 0) V = XOR_q acc_q · H^(63-q).  Level l combines groups of
+// four: lanes 16p+g (level 0), 4p+h (level 1), p (level 2) hold the p-th member, multiply by
+// H^((3-p)·4^l) (tables 2-p, 5-p, 8-p), and XOR across p by two butterflies.
+__device__ __forceinline__ u32x4 flow_tree_r4(u32x4 acc, uint32_t lane) {
+  // the lane-chosen table offsets are made opaque where they are used: left visible, the compiler
+  // hoists the 32 per-lookup addresses of each level out of the unit loop and spills them
+  u32x4 x = shfl4(acc, 4u * (lane & 15u) + (lane >> 4));
+  if (lane < 48u) {
+    uint32_t tb = flow_tab(2u - (lane >> 4));
+    asm volatile("" : "+v"(tb)::"memory");
+    x = gmul_nib(x, tb);
+  }
+  x ^= shfl_xor4(x, 16);
+  x ^= shfl_xor4(x, 32);  // every lane t: A_(t & 15)
+  x = shfl4(x, 4u * (lane & 3u) + ((lane >> 2) & 3u));
+  if (lane < 12u) {
+    uint32_t tb = flow_tab(5u - (lane >> 2));
+    asm volatile("" : "+v"(tb)::"memory");
+    x = gmul_nib(x, tb);
+  }
+  x ^= shfl_xor4(x, 4);
+  x ^= shfl_xor4(x, 8);  // lanes t < 16: B_(t & 3)
+  if (lane < 3u) {
+    uint32_t tb = flow_tab(8u - lane);
+    asm volatile("" : "+v"(tb)::"memory");
+    x = gmul_nib(x, tb);
+  }
+  x ^= shfl_xor4(x, 1);
+  x ^= shfl_xor4(x, 2);  // lane 0: V
+  return x;
+}
+
+template <bool DECRYPT, int NT, bool R4>
+__global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
+  const bool prb = a.probe && threadIdx.x == 0u;
+  if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t nb = a.nb;
+  const int32_t nx = (int32_t)nb + 1;
+  const uint32_t rem = a.len - 16u * (nb ? nb - 1u : 0u);
+  const int32_t C = 64 * (int32_t)a.S;
+  constexpr uint32_t wpb = NT / 64;
+  const uint32_t units = a.nrec * a.nch;
+  // unit u = (record r, chunk i): chunk 0 absorbs the remainder, the others are C X-blocks
+  auto unit_base = [&](uint32_t u, uint32_t& r, uint32_t& i, uint32_t& steps) -> int32_t {
+    r = u / a.nch;
+    i = u - r * a.nch;
+    steps = i == 0u ? (a.r0 + 63u) >> 6 : a.S;
+    return i == 0u ? (int32_t)a.r0 - 64 * (int32_t)steps : nx - (int32_t)(a.nch - i) * C;
+  };
+  auto full_blk = [&](int32_t p) { return p >= 0 && p < (int32_t)nb && (p + 1 < (int32_t)nb || rem == 16u); };
+  auto load_x = [&](const uint8_t* in_rec, int32_t base, uint32_t k) -> u32x4 {
+    const int32_t p = base + 64 * (int32_t)k + (int32_t)lane;
+    return ld_blk(in_rec + 16u * (uint32_t)(full_blk(p) ? p : 0));
+  };
+  // the first unit's first two input rows are requested before the table staging: their HBM
+  // latency overlaps it
+  u32x4 va0 = {0u, 0u, 0u, 0u}, vb0 = {0u, 0u, 0u, 0u};
+  {
+    const uint32_t u = blockIdx.x * wpb + wv;
+    if (u < units) {
+      uint32_t r, i, steps;
+      const int32_t base = unit_base(u, r, i, steps);
+      va0 = load_x(a.in + (uint64_t)r * a.in_stride, base, 0u);
+      vb0 = load_x(a.in + (uint64_t)r * a.in_stride, base, 1u);
+    }
+  }
+  stage_flow<NT, R4>(a);
+  if (prb) a.probe[blockIdx.x * 8u + 1u] = wall_clock64();
+  const RoundKeys rk = a.rk;  // host-keyed: folded round keys in the arguments
+  const RowLanes rl = row_lanes(kGcmRows);
+  const GhashLane gl = ghash_lane();
+  const uint64_t cbits = (uint64_t)a.len * 8u;
+  const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
+  for (uint32_t ub = blockIdx.x * wpb; ub < units; ub += gridDim.x * wpb) {  // workgroup-uniform
+    const uint32_t u = ub + wv;
+    u32x4 pw = {0u, 0u, 0u, 0u};
+    uint32_t r = 0xffffffffu;
+    if (u < units) {  // wave-uniform
+      uint32_t i, steps;
+      const int32_t base = unit_base(u, r, i, steps);
+      const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
+      uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
+      uint32_t n0, n1, n2;
+      gcm_nonce(a, r, !DECRYPT && i == 0u && lane == 0u, n0, n1, n2);
+      auto prefetch = [&](uint32_t k) -> u32x4 { return load_x(in_rec, base, k); };
+      CtrCache cc;
+      uint32_t cc_win = 0xffffffffu;
+      auto keystream = [&](uint32_t ctr) -> u32x4 {
+        const uint32_t w3 = __builtin_bswap32(ctr);
+        if (a.sched & 1024u) return u32x4{w3, n0, n1, n2};  // timing ablation: no AES
+        if ((ctr >> 8) != cc_win) {
+          ctr_cache_fill(rk, rl, n0, n1, n2, w3, cc);
+          cc_win = ctr >> 8;
+        }
+        uint32_t s0, s1, s2, s3;
+        aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
+        return u32x4{s0, s1, s2, s3};
+      };
+      u32x4 acc = {0u, 0u, 0u, 0u};
+      auto consume = [&](uint32_t k, u32x4 v) {
+        const int32_t p = base + 64 * (int32_t)k + (int32_t)lane;
+        const u32x4 ks = keystream(2u + (uint32_t)p);
+        u32x4 x = {0u, 0u, 0u, 0u};
+        if (p >= 0 && p < (int32_t)nb) {
+          uint8_t* op = out_rec + 16u * (uint32_t)p;
+          if (full_blk(p)) {
+            const u32x4 o = v ^ ks;
+            st_blk(op, o);
+            x = DECRYPT ? v : o;
+          } else {
+            const u32x4 pp = load_partial(in_rec + 16u * (uint32_t)p, rem);
+            const u32x4 o = mask_bytes(pp ^ ks, rem);
+            store_partial(op, o, rem);
+            x = DECRYPT ? pp : o;
+          }
+        } else if (p == nx - 1) {
+          x = lenblk;
+        }
+        if constexpr (R4) {
+          if (k == 0u) acc = x;  // wave-uniform; acc was 0
+          else acc = gmul_nib(acc, flow_tab(9u)) ^ x;
+        } else {
+          acc = gmul_byte(acc, gl) ^ x;
+        }
+      };
+      const bool first = ub == blockIdx.x * wpb;
+      u32x4 va = first ? va0 : prefetch(0), vb = first ? vb0 : prefetch(1);
+      uint32_t it = 0;
+      for (uint32_t k = 0; k < steps; k += 2u) {
+        if (a.sched & 1u) rotate_prio(it++);
+        consume(k, va);
+        va = prefetch(k + 2u);
+        if (k + 1u < steps) consume(k + 1u, vb);
+        vb = prefetch(k + 3u);
+      }
+      u32x4 ekj = {0u, 0u, 0u, 0u};
+      if (i == 0u) ekj = keystream(1u);  // E_K(J0) folded into chunk 0's partial
+      if (prb && u == blockIdx.x * wpb) a.probe[blockIdx.x * 8u + 2u] = wall_clock64();
+      if constexpr (R4) {
+        const u32x4 M = a.chw[4u * i + 3u];  // H^(1 + (nch-1-i)C), requested before the tree
+        u32x4 V = (a.sched & 256u) ? acc : flow_tree_r4(acc, lane);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) V[c] = (uint32_t)__builtin_amdgcn_readfirstlane(V[c]);
+        pw = ((a.sched & 512u) ? V ^ M : gmul_wave(V, M)) ^ ekj;
+      } else {
+#pragma unroll
+        for (uint32_t b = 0; b < 4u; ++b) {  // lane tree levels 0..3 (as in gcm_wide_kernel)
+          const u32x4 up = shfl_down4(acc, 1u << b);
+          if ((lane & ((2u << b) - 1u)) == 0u && !(a.sched & 256u)) {
+            asm volatile("" ::: "memory");
+            acc = gmul_nib(acc, kGcmNib + b * 8192u) ^ up;
+          }
+        }
+        u32x4 T[4], M[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) T[j][c] = (uint32_t)__builtin_amdgcn_readlane(acc[c], 16 * j);
+          M[j] = a.chw[4u * i + (uint32_t)j];
+        }
+        pw = ((a.sched & 512u) ? T[0] ^ T[1] ^ T[2] ^ T[3] ^ M[0] : gmul_wave4(T, M)) ^ ekj;
+      }
+      if (prb && u == blockIdx.x * wpb) a.probe[blockIdx.x * 8u + 5u] = wall_clock64();
+    }
+    if (!a.wcnt) {  // partials for gcm_xor_combine_kernel
+      if (u < units && lane == 0u) a.partial[u] = pw;
+      continue;
+    }
+    if constexpr (R4) {
+      if (lane == 0u) {
+        lds_st128(kFlowAgg + 16u * wv, pw);
+        lds_st32(kFlowAgg + 256u + 4u * wv, r);
+      }
+      __syncthreads();
+      const uint32_t l = threadIdx.x;
+      const uint32_t rr = l < wpb ? lds32(kFlowAgg + 256u + 4u * l) : 0xffffffffu;
+      if (rr != 0xffffffffu && (l == 0u || lds32(kFlowAgg + 256u + 4u * (l - 1u)) != rr)) {  // first slot of rr
+        u32x4 x = {0u, 0u, 0u, 0u};
+        uint32_t cnt = 0;
+        for (uint32_t j = l; j < wpb && lds32(kFlowAgg + 256u + 4u * j) == rr; ++j, ++cnt) x ^= lds128(kFlowAgg + 16u * j);
+        uint64_t* ta = reinterpret_cast<uint64_t*>(a.wcnt + 8u * rr + 4u);
+        __hip_atomic_fetch_xor(ta, (uint64_t)x[0] | ((uint64_t)x[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_xor(ta + 1, (uint64_t)x[2] | ((uint64_t)x[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(a.wcnt + 8u * rr, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + cnt == a.nch) {  // every chunk of record rr is in the accumulator
+          const uint64_t lo = __hip_atomic_load(ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t hi = __hip_atomic_load(ta + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(ta, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(ta + 1, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.wcnt + 8u * rr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const u32x4 y = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+          if (!DECRYPT) {
+            st_blk(a.out + (uint64_t)rr * a.out_stride + a.len, y);
+          } else {  // verdict only: the zero-fill of a failed record is zero_failed_kernel's
+            const u32x4 d = ld_blk(a.in + (uint64_t)rr * a.in_stride + a.len) ^ y;
+            a.status[rr] = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+          }
+        }
+      }
+      __syncthreads();  // slots reused by the next round
+    } else {
+      if (u >= units) continue;
+      // publish the partial write-through, count the arrival
+      uint32_t old = 0;
+      if (lane == 0u) {
+        uint64_t* pp = reinterpret_cast<uint64_t*>(a.partial + u);
+        __hip_atomic_store(pp, (uint64_t)pw[0] | ((uint64_t)pw[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pp + 1, (uint64_t)pw[2] | ((uint64_t)pw[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        old = __hip_atomic_fetch_add(a.wcnt + 8u * r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      old = __shfl(old, 0);
+      if (old != a.nch - 1u) continue;  // wave-uniform: not the last chunk of record r to arrive
+      if (lane == 0u) __hip_atomic_store(a.wcnt + 8u * r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      u32x4 y = {0u, 0u, 0u, 0u};
+      const uint64_t* rp = reinterpret_cast<const uint64_t*>(a.partial + (uint64_t)r * a.nch);
+      for (uint32_t k = lane; k < a.nch; k += 64u) {
+        const uint64_t lo = __hip_atomic_load(rp + 2u * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t hi = __hip_atomic_load(rp + 2u * k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        y ^= u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+      }
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) y ^= shfl_xor4(y, m);
+      if (lane == 0u) {
+        uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
+        if (!DECRYPT) {
+          st_blk(out_rec + a.len, y);
+        } else {
+          const u32x4 d = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len) ^ y;
+          a.status[r] = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+        }
+      }
+    }
+  }
+  if (a.probe) {
+    __syncthreads();
+    if (prb) a.probe[blockIdx.x * 8u + 6u] = wall_clock64();
+  }
+}
+
 struct GcmCombineArgs {
   const uint8_t* in;   // open: ct||tag records (for the received tag)
   uint8_t* out;        // seal: ct||tag records (tag written); open: pt records (zeroed on failure)
@@ -555,6 +866,47 @@ __global__ __launch_bounds__(256) void gcm_combine_kernel(GcmCombineArgs a) {
       for (uint32_t i = full + lane; i < a.len; i += 64u) o[i] = 0u;
     }
   }
+}
+
+// Combine of already-weighted partials (wide plan with chunk weights: tag = E_K(J0) folded into
+// chunk 0, so tag = XOR of the record's partials): one 256-thread block per record, every
+// partial load in flight at once (the generic combine's lane loop paid one load latency per 64
+// partials: 8 in sequence for a 1 MiB record), a wave shuffle and an LDS step reduce.
+constexpr uint32_t kXorCombineThreads = 256u;
+template <bool DECRYPT>
+__global__ __launch_bounds__(256) void gcm_xor_combine_kernel(GcmCombineArgs a) {
+  const uint32_t r = blockIdx.x, t = threadIdx.x, lane = t & 63u;
+  const u32x4* part = a.partial + (uint64_t)r * a.nseg;
+  u32x4 y[4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+  uint32_t k = t;
+  for (; k + 3u * 256u < a.nseg; k += 4u * 256u) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] ^= part[k + (uint32_t)j * 256u];
+  }
+  for (; k < a.nseg; k += 256u) y[0] ^= part[k];
+  u32x4 v = y[0] ^ y[1] ^ y[2] ^ y[3];
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) v ^= shfl_xor4(v, m);
+  if (lane == 0u) lds_st128((t >> 6) * 16u, v);
+  __syncthreads();
+  if (t == 0u) {
+    v = lds128(0u) ^ lds128(16u) ^ lds128(32u) ^ lds128(48u);
+    if (!DECRYPT) {
+      st_blk(a.out + (uint64_t)r * a.out_stride + a.len, v);
+    } else {
+      const u32x4 d = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len) ^ v;
+      const uint32_t ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1u : 0u;
+      if (a.status) a.status[r] = (int32_t)ok;
+      lds_st32(64u, ok);
+    }
+  }
+  if (!DECRYPT) return;
+  __syncthreads();
+  if (lds32(64u)) return;
+  uint8_t* o = a.out + (uint64_t)r * a.out_stride;  // zero-fill (aead.h:276-278)
+  const uint32_t full = a.len & ~3u;
+  for (uint32_t i = t * 4u; i < full; i += 256u * 4u) *reinterpret_cast<u32a*>(o + i) = 0u;
+  for (uint32_t i = full + t; i < a.len; i += 256u) o[i] = 0u;
 }
 
 }  // namespace dev

@@ -6,7 +6,8 @@
 // Output layout = DevTables in cmpi_aead.hip: keys[0..43] round keys (folded), keys[48..51] H,
 // H^(2^i), basis chains; then gcm_tables_kernel expands byte tables of H, H^2, H^4, H^64
 // ([v][p], 4096 x 16 B each) and nibble tables of H^1..H^4 and H^(2^b) (512 x 16 B each) —
-// bit-identical to gf128_host.hpp's host builders.  Two launches, ~10 us in all.
+// and the FLOW kernel's nibble tables of H^1,2,3,4,8,12,16,32,48,64 — bit-identical to
+// gf128_host.hpp's host builders.  Two launches, ~10 us in all.
 #pragma once
 #include "aes_device.hpp"
 
@@ -22,20 +23,23 @@ struct KeysetupArgs {
                         // X -> X^(2^i) (key independent, host-built once per process)
   uint32_t* keys;       // out: [0..43] round keys of K' (folded), [48..51] H = E_K'(0)
   u32x4* h2pow;         // out: H^(2^i), i < 32
-  u32x4* chains;        // out: basis chains P·x^i (i < 128) of P = H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
+  u32x4* chains;        // out: basis chains P·x^i (i < 128) of P = H, H^2, H^3, H^4, H^8, H^16, H^32, H^64,
+                        //      H^12, H^48
 };
 
-// The 8 chained multipliers: index -> exponent of H.
+// The 10 chained multipliers: index -> exponent of H.
+constexpr uint32_t kKsChains = 10;
 __host__ __device__ constexpr uint32_t ks_chain_exp(uint32_t j) {
-  return j == 0 ? 1u : j == 1 ? 2u : j == 2 ? 3u : j == 3 ? 4u : j == 4 ? 8u : j == 5 ? 16u : j == 6 ? 32u : 64u;
+  return j == 0 ? 1u : j == 1 ? 2u : j == 2 ? 3u : j == 3 ? 4u : j == 4 ? 8u : j == 5 ? 16u : j == 6 ? 32u
+       : j == 7 ? 64u : j == 8 ? 12u : 48u;
 }
 
 // LDS (dynamic only: offsets are addresses): AES row image @0 (64 KiB), S-box bytes @64K
-// (256 words), then 8 slots: H^(2^i) for i < 7 and H^3 (slot 7).
+// (256 words), then 10 slots: H^(2^i) for i < 7, H^3 (slot 7), H^12 (slot 8), H^48 (slot 9).
 constexpr uint32_t kKsRows = 0u;
 constexpr uint32_t kKsSbox = 65536u;
 constexpr uint32_t kKsPow = kKsSbox + 1024u;
-constexpr uint32_t kKsLds = kKsPow + 8u * 16u;
+constexpr uint32_t kKsLds = kKsPow + 10u * 16u;
 
 // bit k (coefficient of x^k) of a memory-order element
 __device__ __forceinline__ uint32_t gf_bit(u32x4 x, uint32_t k) {
@@ -105,27 +109,30 @@ __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
     }
   }
   __syncthreads();
-  // H^3 = H^2 · H: lane q contributes H·x^q [bit q of H^2] and H·x^(q+64) [bit q+64]
-  if (t < 64u) {
-    const u32x4 H2 = lds128(kKsPow + 16u);
+  // products by one wave each, lane q contributing A·x^q [bit q of B] and A·x^(q+64) [bit q+64]:
+  // wave 0 H^3 = H^2 · H, wave 1 H^12 = H^8 · H^4, wave 2 H^48 = H^32 · H^16
+  if (t < 192u) {
+    const uint32_t w = t >> 6, q = t & 63u;
+    const u32x4 A = lds128(kKsPow + 16u * (w == 0u ? 0u : w == 1u ? 2u : 4u));
+    const u32x4 B = lds128(kKsPow + 16u * (w == 0u ? 1u : w == 1u ? 3u : 5u));
     uint64_t ah, al, bh, bl;
-    gf_split(H, ah, al);
+    gf_split(A, ah, al);
     bh = ah;
     bl = al;
-    gf_mulx_pow(ah, al, t);
-    gf_mulx_pow(bh, bl, t + 64u);
+    gf_mulx_pow(ah, al, q);
+    gf_mulx_pow(bh, bl, q + 64u);
     u32x4 acc = {0u, 0u, 0u, 0u};
-    if (gf_bit(H2, t)) acc ^= gf_join(ah, al);
-    if (gf_bit(H2, t + 64u)) acc ^= gf_join(bh, bl);
+    if (gf_bit(B, q)) acc ^= gf_join(ah, al);
+    if (gf_bit(B, q + 64u)) acc ^= gf_join(bh, bl);
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) acc ^= shfl_xor4(acc, m);
-    if (t == 0u) lds_st128(kKsPow + 16u * 7u, acc);
+    if (q == 0u) lds_st128(kKsPow + 16u * (7u + w), acc);
   }
   __syncthreads();
-  // basis chains: entry (j, i) = P_j · x^i, P_j = H, H^2, H^3, H^4, H^8, H^16, H^32, H^64
-  for (uint32_t e = t; e < 1024u; e += blockDim.x) {
+  // basis chains: entry (j, i) = P_j · x^i, P_j = H, H^2, H^3, H^4, H^8, H^16, H^32, H^64, H^12, H^48
+  for (uint32_t e = t; e < kKsChains * 128u; e += blockDim.x) {
     const uint32_t j = e >> 7, i = e & 127u;
-    const uint32_t slot = j == 2u ? 7u : (j < 2u ? j : j - 1u);
+    const uint32_t slot = j == 2u ? 7u : j >= 8u ? j : (j < 2u ? j : j - 1u);
     uint64_t ph, pl;
     gf_split(lds128(kKsPow + 16u * slot), ph, pl);
     gf_mulx_pow(ph, pl, i);
@@ -143,8 +150,18 @@ struct TablesArgs {
   u32x4* h64;           // 4096
   u32x4* ntab;          // 4 x 512: H^1..H^4
   u32x4* wnib;          // 7 x 512: H^(2^b)
+  u32x4* fnib;          // 10 x 512: H^1, 2, 3, 4, 8, 12, 16, 32, 48, 64 (gcm_flow_kernel, radix-4 tree)
 };
-constexpr uint32_t kTabEntries = 4u * 4096u + 11u * 512u;
+constexpr uint32_t kFlowNib = 10;
+constexpr uint32_t kTabEntries = 4u * 4096u + (11u + kFlowNib) * 512u;
+// exponent of H of FLOW nibble table f, and its basis chain
+__host__ __device__ constexpr uint32_t flow_nib_exp(uint32_t f) {
+  return f == 0 ? 1u : f == 1 ? 2u : f == 2 ? 3u : f == 3 ? 4u : f == 4 ? 8u : f == 5 ? 12u : f == 6 ? 16u
+       : f == 7 ? 32u : f == 8 ? 48u : 64u;
+}
+__host__ __device__ constexpr uint32_t flow_nib_chain(uint32_t f) {
+  return f < 5u ? f : f == 5u ? 8u : f == 6u ? 5u : f == 7u ? 6u : f == 8u ? 9u : 7u;
+}
 
 __global__ __launch_bounds__(256) void gcm_tables_kernel(TablesArgs a) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -166,14 +183,15 @@ __global__ __launch_bounds__(256) void gcm_tables_kernel(TablesArgs a) {
   const uint32_t f = e - 4u * 4096u;
   const uint32_t t = f >> 9, row = (f >> 4) & 31u, v = f & 15u, p = row >> 1, sh = (row & 1u) ? 0u : 4u;
   const uint32_t b = t - 4u;
-  const uint32_t ch = t < 4u ? t : (b == 0u ? 0u : b == 1u ? 1u : b + 1u);
+  const uint32_t ch = t < 4u ? t : t >= 11u ? flow_nib_chain(t - 11u) : (b == 0u ? 0u : b == 1u ? 1u : b + 1u);
   const u32x4* c = a.chains + ch * 128u + 8u * p + 7u - sh;
   u32x4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     if (v & (1u << k)) acc ^= *(c - k);
   if (t < 4u) a.ntab[f] = acc;
-  else a.wnib[f - 4u * 512u] = acc;
+  else if (t < 11u) a.wnib[f - 4u * 512u] = acc;
+  else a.fnib[f - 11u * 512u] = acc;
 }
 
 }  // namespace dev

@@ -47,6 +47,13 @@ void* cmpi_debug_event_new(void);
 int cmpi_debug_event_record(void* ev, void* stream);
 float cmpi_debug_event_ms(void* a, void* b);
 void cmpi_debug_event_free(void* ev);
+/* FLOW wide GCM kernel (host-keyed, few long records): threads per workgroup 512 / 1024, or 0
+ * for the round-1 gcm_wide_kernel; flags (default 1): bit 0 combine fused (last arriver), else a
+ * separate gcm_xor_combine_kernel launch; bits 1-3 timing ablations that skip the lane tree (2),
+ * the chunk-weight product (4), the AES (8) — outputs WRONG, for tools/ab_flow.py only; bit 4
+ * the round-2 first form (byte-table Horner, radix-2 tree, gmul_wave4) instead of radix-4; bit 5
+ * keeps `threads` even where the planner would pick 512-thread workgroups for few chunks. */
+void cmpi_debug_set_flow(int threads, int fused);
 /* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}; a wide plan reports
  * L = 64, nseg = chunks per record, G = X-blocks per chunk (64*steps). */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);

@@ -28,6 +28,7 @@ def _auto_plan():
     aead.force_plan(0, 0)
     aead.force_wide(0, 0)
     aead.set_wide_chw(True)
+    aead.set_flow(1024, 0)
 
 
 def gpu_seal(ctx, nonces: np.ndarray, pt: np.ndarray) -> np.ndarray:
@@ -204,6 +205,35 @@ def test_wide_decomposition(n, nrec, steps, chw):
     wbuf = dev(wire)
     ctx.seal_batch(wbuf[12:], dev(pt), wbuf, n, nrec, out_stride=stride, nonce_stride=stride)
     assert np.array_equal(host(wbuf).reshape(nrec, stride)[:, 12:], want)
+
+
+@pytest.mark.parametrize("threads,flags", [(1024, 0), (512, 32), (1024, 32), (1024, 1), (512, 33), (1024, 16),
+                                           (1024, 17), (1024, 48), (1024, 49)])
+@pytest.mark.parametrize("n,nrec,steps", [(64 * 16 * 3 - 16, 11, 1), (4097, 5, 2), (1 << 20, 2, 0)])
+def test_flow_kernel_forms(threads, flags, n, nrec, steps):
+    """gcm_flow_kernel in each form — radix-4 tree (nibble tables H^1..H^64, one chunk-weight
+    product) or the round-2 first form (byte-table Horner, radix-2 tree, 4 products); 512 or 1024
+    threads; partials combined by gcm_xor_combine_kernel or fused (per-workgroup XOR then 8-B agent
+    atomics into the record's accumulator, last adder writes the tag).  3-chunk records put up to
+    six records in one workgroup.  Two seals back to back (the fused counters and accumulators
+    must return to zero), a forged record, and a context re-keyed on the device (tables rebuilt
+    by gcm_tables_kernel, bit-identical to the host build)."""
+    aead.force_wide(1, steps)
+    aead.set_flow(threads, flags)
+    key2 = bytes(range(100, 116))
+    ctx = aead.AeadCtx(KEY)
+    pt = records(0x5100 + n, nrec, n)
+    nonces = random_nonces(0x5200 + n, nrec)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    for _ in range(2):
+        assert np.array_equal(gpu_seal(ctx, nonces, pt), want), aead.gcm_plan(ctx, n, nrec)
+    forged = want.copy()
+    forged[1, n // 3] ^= 0x40
+    back, st = gpu_open(ctx, nonces, forged)
+    assert list(st) == [1] + [0] + [1] * (nrec - 2)
+    assert not back[1].any() and np.array_equal(back[0], pt[0]) and np.array_equal(back[2:], pt[2:])
+    ctx.rekey(key2)
+    assert np.array_equal(gpu_seal(ctx, nonces, pt), oracle.gcm_seal_batch(key2, nonces, pt))
 
 
 @pytest.mark.parametrize("nrec,segments", [(3, 0), (2, 700), (1, 2)])
