@@ -113,6 +113,8 @@ struct HostPipe {
   size_t cap = 0;
   int32_t* hst = nullptr;   // pinned per-record open status of the whole batch
   size_t hst_cap = 0;
+  uint8_t* dbounce = nullptr;  // pinned: direct path's packed pageable records, nonces, statuses
+  size_t dcap = 0;
   bool init = false;
 };
 
@@ -796,13 +798,97 @@ void par_copy_records(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t sp
   for (auto& x : th) x.join();
 }
 
+// Device address of page-locked host memory (the kernel reads / writes it over PCIe), or null.
+void* pinned_dev_ptr(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
+  const uintptr_t off = at.hostPointer ? (uintptr_t)p - (uintptr_t)at.hostPointer : 0;
+  return (uint8_t*)at.devicePointer + off;
+}
+
+// Wait for a stream by polling it (an MPI progress loop's busy wait): the blocking
+// hipStreamSynchronize sleeps and adds its wake-up latency to every small message.
+std::atomic<int> g_host_spin{1};
+hipError_t spin_sync(hipStream_t st) {
+  if (!g_host_spin.load()) return hipStreamSynchronize(st);
+  for (;;) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e != hipErrorNotReady) return e;
+  }
+}
+
+// Direct host path for small batches (a single MPI message, an EVP call): no DMA launches and no
+// cross-stream events — the kernel reads the records from and writes them to page-locked host
+// memory itself (zero-copy over PCIe), nonces and statuses in a pinned bounce buffer, pageable
+// records packed / unpacked through it on the CPU.  One launch (+ the combine) and one stream
+// synchronisation per call, where the pipeline pays H2D + kernel + D2H + 3 stream joins.
+std::atomic<size_t> g_host_direct{((size_t)2 << 20) + 64};  // largest in+out bytes taken direct (0 = never)
+
+template <bool DEC, bool OCB>
+int host_direct(const cmpi_ctx* c, HostPipe& P, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
+                const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status) {
+  auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
+  void* din = in_rec ? pinned_dev_ptr(in) : nullptr;
+  void* dout = out_rec ? pinned_dev_ptr(out) : nullptr;
+  const size_t bi = in_rec && !din ? up16(in_rec * nrec) : 0, bo = out_rec && !dout ? up16(out_rec * nrec) : 0;
+  const size_t need = bi + bo + up16(16 * nrec) + up16(4 * nrec) + 64;
+  if (P.dcap < need) {
+    HIP_TRY(hipStreamSynchronize(P.s[1]));
+    if (P.dbounce) (void)hipHostFree(P.dbounce);
+    P.dbounce = nullptr;
+    P.dcap = 0;
+    const size_t cap = std::max<size_t>(need, (size_t)1 << 20);
+    if (hipHostMalloc((void**)&P.dbounce, cap, hipHostMallocDefault) != hipSuccess)
+      return fail(CMPI_ENOMEM, "hipHostMalloc bounce failed");
+    P.dcap = cap;
+  }
+  uint8_t* B = P.dbounce;
+  uint8_t* dB = (uint8_t*)pinned_dev_ptr(B);
+  if (!dB) return fail(CMPI_EHIP, "bounce buffer has no device address");
+  size_t istr = in_stride, ostr = out_stride;
+  if (!din) {  // pageable (or empty) input records: packed into the bounce buffer
+    if (in_rec) par_copy_records(B, in_rec, in, in_stride, in_rec, nrec);
+    din = dB;
+    istr = std::max<size_t>(in_rec, 1);
+  }
+  uint8_t* hout = nullptr;
+  if (!dout) {
+    hout = B + bi;
+    dout = dB + bi;
+    ostr = std::max<size_t>(out_rec, 1);
+  }
+  uint8_t* hn = B + bi + bo;
+  for (size_t i = 0; i < nrec; ++i) memcpy(hn + 16 * i, nonces + i * nonce_stride, 12);
+  int32_t* hst = reinterpret_cast<int32_t*>(hn + up16(16 * nrec));
+  int32_t* dst = reinterpret_cast<int32_t*>(dB + (bi + bo + up16(16 * nrec)));
+  int rc = OCB ? ocb_batch<DEC>(c, (uint8_t*)dout, ostr, (const uint8_t*)din, istr, dB + bi + bo, 16, len, nrec,
+                               DEC ? dst : nullptr, nullptr, P.s[1])
+               : gcm_batch<DEC>(c, (uint8_t*)dout, ostr, (const uint8_t*)din, istr, dB + bi + bo, 16, len, nrec,
+                               DEC ? dst : nullptr, nullptr, P.s[1]);
+  if (rc) return rc;
+  HIP_TRY(spin_sync(P.s[1]));
+  if (hout && out_rec) par_copy_records(out, out_stride, hout, out_rec, out_rec, nrec);
+  if (DEC) {
+    size_t bad = 0;
+    for (size_t i = 0; i < nrec; ++i) bad += hst[i] != 1;
+    if (status) memcpy(status, hst, 4 * nrec);
+    if (bad) return fail(CMPI_EAUTH, "%zu of %zu records failed authentication", bad, nrec);
+  }
+  return CMPI_OK;
+}
+
 template <bool DEC, bool OCB>
 int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
               const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status) {
   if (!c) return fail(CMPI_EINVAL, "null ctx");
   if (nrec == 0) return CMPI_OK;
-  if (!out || !in || !nonces) return fail(CMPI_EINVAL, "null buffer");
   const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
+  if ((!out && out_rec) || (!in && in_rec) || !nonces) return fail(CMPI_EINVAL, "null buffer");
   if (nrec > 1 && (in_stride < in_rec || out_stride < out_rec || nonce_stride < 12))
     return fail(CMPI_EINVAL, "stride smaller than record");
   if (nrec == 1) in_stride = in_rec, out_stride = out_rec, nonce_stride = 12;
@@ -818,6 +904,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
     P.init = true;
   }
+  if (nrec * (in_rec + out_rec) <= g_host_direct.load())
+    return host_direct<DEC, OCB>(c, P, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, status);
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const bool in_pinned = in_rec && is_pinned(in), out_pinned = out_rec && is_pinned(out);
   // Device pitch = the user's stride when one flat DMA can move the chunk: inputs may carry
@@ -1172,6 +1260,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
     if (P.buf) (void)hipFree(P.buf);
     if (P.hbuf) (void)hipHostFree(P.hbuf);
     if (P.hst) (void)hipHostFree(P.hst);
+    if (P.dbounce) (void)hipHostFree(P.dbounce);
   }
   if (c->dt) (void)hipFree(c->dt);
   memset(c->key, 0, 16);
@@ -1206,6 +1295,9 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
 }
 
 void cmpi_debug_set_wide_chw(int on) { g_wide_chw.store(on ? 1 : 0); }
+void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
+void cmpi_debug_set_host_spin(int on) { g_host_spin.store(on ? 1 : 0); }
+
 void cmpi_debug_set_flow(int threads, int fused) {
   g_flow_nt.store(threads == 512 || threads == 1024 ? threads : (threads == 0 ? 0 : 1024));
   g_flow_fused.store(fused);  // bit 0 fused combine; bits 1-3 timing ablations (wrong output); bit 4 !R4

@@ -54,6 +54,12 @@ void cmpi_debug_event_free(void* ev);
  * the round-2 first form (byte-table Horner, radix-2 tree, gmul_wave4) instead of radix-4; bit 5
  * keeps `threads` even where the planner would pick 512-thread workgroups for few chunks. */
 void cmpi_debug_set_flow(int threads, int fused);
+/* Host-memory calls (cmpi_*_host) up to `bytes` of input + output records run the direct path
+ * (kernel on page-locked host memory, no DMA); larger ones the 3-stream pipeline.  0 = never. */
+void cmpi_debug_set_host_direct(size_t bytes);
+/* Direct host path: wait for the kernel by polling the stream (1, default) or by a blocking
+ * hipStreamSynchronize (0). */
+void cmpi_debug_set_host_spin(int on);
 /* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}; a wide plan reports
  * L = 64, nseg = chunks per record, G = X-blocks per chunk (64*steps). */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);

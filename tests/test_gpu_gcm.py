@@ -18,6 +18,7 @@ from tests.gpu_util import dev, empty, host, status_buf
 pytestmark = pytest.mark.gpu
 
 KEY = bytes.fromhex("000102030405060708090a0b0c0d0e0f")
+DIRECT_DEFAULT = (2 << 20) + 64  # cmpi_aead.hip g_host_direct
 
 
 @pytest.fixture(autouse=True)
@@ -29,6 +30,7 @@ def _auto_plan():
     aead.force_wide(0, 0)
     aead.set_wide_chw(True)
     aead.set_flow(1024, 0)
+    aead.N.lib().cmpi_debug_set_host_direct(DIRECT_DEFAULT)
 
 
 def gpu_seal(ctx, nonces: np.ndarray, pt: np.ndarray) -> np.ndarray:
@@ -291,6 +293,44 @@ def test_config2_full_batch_properties():
     assert np.array_equal(ct.view(nrec, n + 16).cpu().numpy()[idx], want)
 
 
+@pytest.mark.parametrize("n,nrec", [(0, 1), (1, 1), (777, 20), (65536, 1), (1 << 20, 1), (100000, 3)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_direct_single_messages(n, nrec, pinned):
+    """Single MPI messages through cmpi_gcm_seal_host / open_host (the EVP drop-in's and the 600
+    path's call) on the direct path: bit-exact vs the oracle, forged tag -> CMPI_EAUTH, status 0
+    and zero-filled plaintext (aead.h:276-278)."""
+    import torch
+
+    pt = records(0x6100 + n, nrec, n)
+    nonces = random_nonces(0x6200 + n, nrec)
+    ctx = aead.AeadCtx(KEY)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    L = aead.N.lib()
+    if pinned:
+        tp = torch.from_numpy(pt.reshape(-1).copy()).pin_memory()
+        tc = torch.empty(nrec * (n + 16), dtype=torch.uint8).pin_memory()
+        tb = torch.empty(max(nrec * n, 1), dtype=torch.uint8).pin_memory()
+        pp, cp, bp = tp.data_ptr(), tc.data_ptr(), tb.data_ptr()
+        ct_view = lambda: tc.numpy().reshape(nrec, n + 16)  # noqa: E731
+        back_view = lambda: tb.numpy()[: nrec * n].reshape(nrec, n)  # noqa: E731
+    else:
+        cbuf = np.zeros((nrec, n + 16), np.uint8)
+        bbuf = np.zeros((nrec, max(n, 1)), np.uint8)
+        pp, cp, bp = pt.ctypes.data, cbuf.ctypes.data, bbuf.ctypes.data
+        ct_view = lambda: cbuf  # noqa: E731
+        back_view = lambda: bbuf[:, :n]  # noqa: E731
+    aead.N.check(L.cmpi_gcm_seal_host(ctx.handle, cp, n + 16, pp, max(n, 1), nonces.ctypes.data, 12, n, nrec))
+    assert np.array_equal(ct_view(), want)
+    st = np.zeros(nrec, np.int32)
+    aead.N.check(L.cmpi_gcm_open_host(ctx.handle, bp, max(n, 1), cp, n + 16, nonces.ctypes.data, 12, n, nrec,
+                                      st.ctypes.data))
+    assert (st == 1).all() and np.array_equal(back_view(), pt)
+    ct_view()[nrec - 1, -1] ^= 1
+    rc = L.cmpi_gcm_open_host(ctx.handle, bp, max(n, 1), cp, n + 16, nonces.ctypes.data, 12, n, nrec, st.ctypes.data)
+    assert rc == aead.N.CMPI_EAUTH and st[nrec - 1] == 0 and (st[: nrec - 1] == 1).all()
+    assert not back_view()[nrec - 1].any()
+
+
 def test_host_staging_api():
     n, nrec = 777, 20
     pt = records(3, nrec, n)
@@ -425,11 +465,14 @@ def test_device_keyed_ctx_rejects_ctr():
     torch.cuda.synchronize()  # the key-setup kernel is asynchronous
 
 
+@pytest.mark.parametrize("direct", [0, 1 << 30])
 @pytest.mark.parametrize("out_pad", [0, 28])
-def test_host_pipeline_pinned_in_and_out(out_pad):
+def test_host_pipeline_pinned_in_and_out(out_pad, direct):
     """Registered host buffers on both sides move by flat DMA (device pitch = user stride) when
     the output is dense; a gapped output (the wire layout's nonce between records) must keep
-    the caller's gap bytes."""
+    the caller's gap bytes.  direct: the kernel reads / writes the registered pages itself
+    (their device address from hipPointerGetAttributes) at the caller's strides."""
+    aead.N.lib().cmpi_debug_set_host_direct(direct)
     n, nrec = 1000, 257
     pt = records(0x7171 + out_pad, nrec, n)
     nonces = random_nonces(0x7172, nrec)
@@ -460,10 +503,14 @@ def test_host_pipeline_pinned_in_and_out(out_pad):
 
 
 @pytest.mark.parametrize("alg", ["aes-128-gcm", "aes-128-ocb"])
-@pytest.mark.parametrize("chunk", [4096, 65536, 0])
+@pytest.mark.parametrize("chunk", [4096, 65536, 0, -1])
 def test_host_pipeline_chunks(alg, chunk):
     """The pipelined host path (3 streams, 2 staging slots) across many chunks, ragged last chunk,
-    forged records reported per record and zero-filled, for pinned (registered) and pageable."""
+    forged records reported per record and zero-filled, for pinned (registered) and pageable.
+    chunk -1: the direct path (kernel on page-locked host memory, pageable records packed through
+    the pinned bounce buffer) on the same cases."""
+    aead.N.lib().cmpi_debug_set_host_direct(1 << 30 if chunk < 0 else 0)
+    chunk = max(chunk, 0)
     n, nrec = 1000, 301
     pt = records(0x5151 + chunk, nrec, n)
     nonces = random_nonces(0x5152, nrec)
