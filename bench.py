@@ -165,13 +165,20 @@ class KernelEvents:
             self.L.cmpi_debug_event_free(e)
 
 
-def time_steps(w: Workload, steps: int, warmup: int, barrier):
+def time_steps(w: Workload, steps: int, warmup: int, barrier, warmup_s: float = 0.0):
     """Returns (wall seconds for `steps` steps, avg seal kernel ms, avg open kernel ms) —
     kernel times from HIP events recorded on the stream the kernels are launched on, around every
-    seal and open launch of the timed region (fence-free events, KernelEvents)."""
-    for _ in range(warmup):
+    seal and open launch of the timed region (fence-free events, KernelEvents).  The warm-up is
+    `warmup` steps and, when warmup_s > 0, at least that many seconds of them (the extras run
+    after the CPU baseline has left the GPU idle for seconds: clocks ramp back up first)."""
+    t_w = time.perf_counter()
+    i = 0
+    while i < warmup or time.perf_counter() - t_w < warmup_s:
         w.seal()
         w.open()
+        i += 1
+        if warmup_s and i % 8 == 0:
+            torch.cuda.synchronize(w.dev)
     torch.cuda.synchronize(w.dev)
     assert w.verify(), "round trip failed in warm-up"
     stream = torch.cuda.current_stream(w.dev).cuda_stream
@@ -853,7 +860,7 @@ def main() -> None:
         for name in ("gcm4k", "ocb1m", "ctr1g", "alltoall"):
             try:
                 we = Workload(name, local, seed=77)
-                wl, s_ms, o_ms = time_steps(we, EXTRA_STEPS, EXTRA_WARMUP, barrier)
+                wl, s_ms, o_ms = time_steps(we, EXTRA_STEPS, EXTRA_WARMUP, barrier, warmup_s=0.3)
                 extras[name] = {"seal_open_GiBps": round(we.n * we.nrec * EXTRA_STEPS / wl / GIB, 2),
                                 "seal_GiBps": round(we.n * we.nrec / (s_ms * 1e-3) / GIB, 2),
                                 "open_GiBps": round(we.n * we.nrec / (o_ms * 1e-3) / GIB, 2),

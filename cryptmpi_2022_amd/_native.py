@@ -114,6 +114,7 @@ _SIGS = {
     "cmpi_debug_set_flow": ([_I, _I], None),
     "cmpi_debug_set_host_direct": ([_S], None),
     "cmpi_debug_set_host_spin": ([_I], None),
+    "cmpi_debug_set_gcm_mem": ([_I], None),
     "cmpi_debug_event_new": ([], _P),
     "cmpi_debug_event_record": ([_P, _P], _I),
     "cmpi_debug_event_ms": ([_P, _P], ctypes.c_float),

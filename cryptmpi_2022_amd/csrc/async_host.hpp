@@ -108,6 +108,61 @@ void req_release(cmpi_req* r) {
   delete r;
 }
 
+// Small requests (<= g_host_direct bytes in + out, cmpi_aead.hip): the kernel reads and writes
+// page-locked user buffers itself, pageable ones go through the request's pinned buffer, nonces
+// and statuses live there too; device memory only for the kernel workspace.  No DMA launches.
+template <bool DEC, bool OCB, class Bail>
+int direct_begin(const cmpi_ctx* c, StagePool& P, cmpi_req* r, uint8_t* out, size_t out_stride, const uint8_t* in,
+                 size_t in_stride, const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, cmpi_req** req,
+                 Bail& bail) {
+  auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
+  void* din = in_rec ? pinned_dev_ptr(in) : nullptr;
+  void* dout = out_rec ? pinned_dev_ptr(out) : nullptr;
+  size_t ws = 0;
+  if (OCB) {
+    const OcbPlan pl = plan_ocb(c, len, nrec);
+    ws = (size_t)nrec * pl.nchunks * 16 + nrec * 16 + nrec * 4;
+  } else {
+    ws = gcm_ws_bytes(c, plan_gcm(c, len, nrec), nrec);
+  }
+  int rc;
+  if (ws && (rc = pool_take(P, false, up16(ws) + 16, &r->dbuf, &r->dcap))) return bail(rc);
+  const size_t bi = !din ? up16(in_rec * nrec) : 0, bo = !dout ? up16(out_rec * nrec) : 0;
+  const size_t h_in = 0, h_out = bi, h_n = bi + bo, h_st = h_n + up16(16 * nrec), h_total = h_st + up16(4 * nrec) + 16;
+  if ((rc = pool_take(P, true, h_total, &r->hbuf, &r->hcap))) return bail(rc);
+  uint8_t* H = (uint8_t*)r->hbuf;
+  uint8_t* dH = (uint8_t*)pinned_dev_ptr(H);
+  if (!dH) return bail(fail(CMPI_EHIP, "staging buffer has no device address"));
+  size_t istr = in_stride, ostr = out_stride;
+  if (!din) {
+    if (in_rec) par_copy_records(H + h_in, in_rec, in, in_stride, in_rec, nrec);
+    din = dH + h_in;
+    istr = std::max<size_t>(in_rec, 1);
+  }
+  const bool unpack = !dout && out_rec;
+  if (!dout) {
+    dout = dH + h_out;
+    ostr = std::max<size_t>(out_rec, 1);
+  }
+  for (size_t i = 0; i < nrec; ++i) memcpy(H + h_n + 16 * i, nonces + i * nonce_stride, 12);
+  int32_t* dst = DEC ? (int32_t*)(dH + h_st) : nullptr;
+  void* wsp = ws ? r->dbuf : nullptr;
+  rc = OCB ? ocb_batch<DEC>(c, (uint8_t*)dout, ostr, (const uint8_t*)din, istr, dH + h_n, 16, len, nrec, dst, wsp, r->st)
+           : gcm_batch<DEC>(c, (uint8_t*)dout, ostr, (const uint8_t*)din, istr, dH + h_n, 16, len, nrec, dst, wsp, r->st);
+  if (rc) return bail(rc);
+  HIP_TRY(hipEventRecord(r->done, r->st));
+  r->unpack = unpack;
+  r->user_out = out;
+  r->out_stride = out_stride;
+  r->out_rec = out_rec;
+  r->op = ostr;
+  r->h_out = H + h_out;
+  r->h_status = (int32_t*)(H + h_st);
+  *req = r;
+  return CMPI_OK;
+}
+
 template <bool DEC, bool OCB>
 int host_begin(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
                const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status, cmpi_req** req) {
@@ -144,6 +199,8 @@ int host_begin(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t
   if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess)
     return bail(fail(CMPI_EHIP, "event create failed"));
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  if (nrec && nrec * (in_rec + out_rec) <= g_host_direct.load())
+    return direct_begin<DEC, OCB>(c, P, r, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, req, bail);
   const bool in_pinned = in_rec && is_pinned(in), out_pinned = out_rec && is_pinned(out);
   const bool in_flat = in_pinned && (nrec == 1 || in_stride <= in_rec + 64);
   const bool out_flat = out_pinned && (nrec == 1 || out_stride == out_rec);

@@ -249,6 +249,7 @@ struct GcmPlan {
 // test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
 std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
+std::atomic<int> g_gcm_mem{0};        // lane kernel record-data cache policy: bit 0 nt loads, bit 1 nt stores
 std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4/6
 std::atomic<int> g_wide_chw{1};       // wide plan, host-keyed: barrier-free FLOW kernel with chunk weights (1) or weights in the combine (0)
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
@@ -439,6 +440,12 @@ int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size
     case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 3>; break;
     case 4: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 4>; break;
     case 6: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 6>; break;
+    default: break;
+  }
+  switch (g_gcm_mem.load()) {  // non-temporal record loads (1) / stores (2) / both (3)
+    case 1: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 2, 1>; break;
+    case 2: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 2, 2>; break;
+    case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 2, 3>; break;
     default: break;
   }
   if constexpr (!DEC) {
@@ -1296,6 +1303,7 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
 
 void cmpi_debug_set_wide_chw(int on) { g_wide_chw.store(on ? 1 : 0); }
 void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
+void cmpi_debug_set_gcm_mem(int mode) { g_gcm_mem.store(mode & 3); }
 void cmpi_debug_set_host_spin(int on) { g_host_spin.store(on ? 1 : 0); }
 
 void cmpi_debug_set_flow(int threads, int fused) {

@@ -79,6 +79,17 @@ __device__ __forceinline__ RoundKeys load_round_keys(const RoundKeys& arg, const
 
 __device__ __forceinline__ u32x4 ld_blk(const uint8_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
 __device__ __forceinline__ void st_blk(uint8_t* p, u32x4 v) { *reinterpret_cast<u32x4a*>(p) = v; }
+// record data streamed once (MEM bit 0: loads, bit 1: stores) with the non-temporal policy
+template <int MEM>
+__device__ __forceinline__ u32x4 ld_rec(const uint8_t* p) {
+  if constexpr (MEM & 1) return __builtin_nontemporal_load(reinterpret_cast<const u32x4a*>(p));
+  else return ld_blk(p);
+}
+template <int MEM>
+__device__ __forceinline__ void st_rec(uint8_t* p, u32x4 v) {
+  if constexpr (MEM & 2) __builtin_nontemporal_store(v, reinterpret_cast<u32x4a*>(p));
+  else st_blk(p, v);
+}
 
 // Record r's 96-bit nonce as three LE words (see GcmArgs::nmode); `writer` (one lane of the
 // record, seal only) also writes the nonce / 5-byte prefix the framing puts on the wire.
@@ -131,7 +142,7 @@ __host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return kGcmNib + (
 // ABL (timing ablation, wrong results): bit 0 = GHASH multiply skipped, bit 1 = AES skipped
 // (keystream = counter block), bit 2 = record data addressed as one coalesced stream per wave
 // (same bytes moved, dense layouts only).
-template <int L, bool DECRYPT, int ABL = 0, int PF = 2>
+template <int L, bool DECRYPT, int ABL = 0, int PF = 2, int MEM = 0>
 __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   stage_copy(a.htab, 0u, 4096u);
   stage_rows(a.te0, kGcmRows);
@@ -185,7 +196,7 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
     auto prefetch = [&](uint32_t u) -> u32x4 {
       if (ABL & 4) return full_blk(u) ? ld_blk(a.in + abl_off(u)) : u32x4{0u, 0u, 0u, 0u};
       const uint32_t j = full_blk(u) ? x0 + u : 0u;
-      return ld_blk(pf_base + 16u * j);
+      return ld_rec<MEM>(pf_base + 16u * j);
     };
     // slot u with keystream ks and its prefetched input block v
     auto consume = [&](uint32_t u, u32x4 ks, u32x4 v) {
@@ -199,7 +210,7 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
         uint8_t* op = (ABL & 4) ? a.out + abl_off(u) : out_rec + 16u * j;
         if (full_blk(u)) {
           const u32x4 o = v ^ ks;
-          st_blk(op, o);
+          st_rec<MEM>(op, o);
           x = DECRYPT ? v : o;
         } else {
           const u32x4 p = load_partial(in_rec + 16u * j, rem);

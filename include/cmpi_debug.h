@@ -57,6 +57,8 @@ void cmpi_debug_set_flow(int threads, int fused);
 /* Host-memory calls (cmpi_*_host) up to `bytes` of input + output records run the direct path
  * (kernel on page-locked host memory, no DMA); larger ones the 3-stream pipeline.  0 = never. */
 void cmpi_debug_set_host_direct(size_t bytes);
+/* GCM lane-group kernel: record data loaded (bit 0) / stored (bit 1) with the non-temporal policy. */
+void cmpi_debug_set_gcm_mem(int mode);
 /* Direct host path: wait for the kernel by polling the stream (1, default) or by a blocking
  * hipStreamSynchronize (0). */
 void cmpi_debug_set_host_spin(int on);

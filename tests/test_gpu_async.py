@@ -17,13 +17,25 @@ pytestmark = pytest.mark.gpu
 KEY = bytes(range(16))
 
 
+DIRECT_DEFAULT = (2 << 20) + 64  # cmpi_aead.hip g_host_direct
+
+
+@pytest.fixture(params=[DIRECT_DEFAULT, 0], ids=["direct", "dma"])
+def path(request):
+    """Requests up to the threshold run the direct path (kernel on page-locked host memory);
+    threshold 0 sends every request through H2D / kernel / D2H DMA."""
+    N.lib().cmpi_debug_set_host_direct(request.param)
+    yield request.param
+    N.lib().cmpi_debug_set_host_direct(DIRECT_DEFAULT)
+
+
 def _buf(shape, pinned: bool):
     if pinned:
         return torch.empty(shape, dtype=torch.uint8, pin_memory=True).numpy()
     return np.empty(shape, np.uint8)
 
 
-def test_64_outstanding_seal_then_open():
+def test_64_outstanding_seal_then_open(path):
     ctx = aead.AeadCtx(KEY)
     rng = random.Random(64)
     jobs = []
@@ -72,7 +84,7 @@ def test_64_outstanding_seal_then_open():
             assert rc == N.CMPI_OK and (st == 1).all() and np.array_equal(back, pt), i
 
 
-def test_async_ocb_and_overlap_with_device_work():
+def test_async_ocb_and_overlap_with_device_work(path):
     ctx = aead.AeadCtx(KEY, "aes-128-ocb")
     reqs = []
     for i in range(8):
