@@ -601,6 +601,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
   }
   const size_t lds = cmpi::dev::gcm_lds_bytes(p.L);
+  a.probe = g_wide_probe.load();
   const uint64_t want = ((uint64_t)a.ngroups * p.L + kGcmThreads - 1) / kGcmThreads;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->ncu));
   int rc;
@@ -1288,7 +1289,7 @@ int cmpi_host_unregister(void* ptr) {
   return CMPI_OK;
 }
 
-void cmpi_debug_set_sched(int mode) { g_sched.store(mode & 7); }
+void cmpi_debug_set_sched(int mode) { g_sched.store(mode & (7 | 4096 | 8192)); }
 void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)16 << 20)); }
 void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 15); }
 

@@ -144,10 +144,13 @@ __host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return kGcmNib + (
 // (same bytes moved, dense layouts only).
 template <int L, bool DECRYPT, int ABL = 0, int PF = 2, int MEM = 0>
 __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
+  const bool prb = a.probe && threadIdx.x == 0u;  // diagnostics: workgroup start / staged / end
+  if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
   stage_copy(a.htab, 0u, 4096u);
   stage_rows(a.te0, kGcmRows);
   if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)L * 512u);
   __syncthreads();
+  if (prb) a.probe[blockIdx.x * 8u + 1u] = wall_clock64();
   if (ABL & 8) {  // prologue only (table staging cost)
     if (threadIdx.x == 0 && a.nrec == 0xFFFFFFFFu) a.out[0] = (uint8_t)lds32(0u);
     return;
@@ -179,6 +182,20 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
 
     u32x4 acc = {0u, 0u, 0u, 0u};
     u32x4 ekj0 = {0u, 0u, 0u, 0u};
+    // Output-aligned windows (a.sched & 8192): at loop step i the group's L lanes own slots
+    // [L*i - phi, L*i - phi + L - 1], phi putting every window's 16L output bytes on a 16L-byte
+    // boundary (dense ct||tag records are n+16 apart: without it each step's stores straddle two
+    // 64-B sectors, written back twice).  Lane q then owns the slots u = qs (mod L).  Seal of a
+    // one-segment record with a whole last block also holds back the data blocks of the window
+    // that holds the tag and stores them with the tag in one instruction.
+    const bool aligned = (a.sched & 8192u) != 0u;
+    const uint32_t phi = aligned ? ((uint32_t)(reinterpret_cast<uintptr_t>(out_rec) >> 4) + x0) & (uint32_t)(L - 1) : 0u;
+    const uint32_t qs = (q + (uint32_t)L - phi) & (uint32_t)(L - 1);
+    const bool defer = !DECRYPT && aligned && L > 1 && a.nseg == 1 && rem == 16u && nb > 0u;
+    const uint32_t tslot = nxs - 1u;  // the length block's slot: the tag's position
+    const uint32_t wlast = ((tslot + phi) & ~(uint32_t)(L - 1)) - phi;  // first slot of its window (>= 0 or wraps)
+    u32x4 pend = {0u, 0u, 0u, 0u};
+    uint8_t* pend_at = nullptr;
     // Input blocks are software-prefetched two slots ahead: loads and stores share vmcnt, so a
     // load consumed right after issue would also wait for the previous slot's store to retire.
     auto full_blk = [&](uint32_t u) { return u < nxs && x0 + u < nb && (x0 + u + 1u < nb || rem == 16u); };
@@ -210,7 +227,12 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
         uint8_t* op = (ABL & 4) ? a.out + abl_off(u) : out_rec + 16u * j;
         if (full_blk(u)) {
           const u32x4 o = v ^ ks;
-          st_rec<MEM>(op, o);
+          if (defer && u + phi >= wlast + phi && u < tslot) {  // held for the tag's store
+            pend = o;
+            pend_at = op;
+          } else {
+            st_rec<MEM>(op, o);
+          }
           x = DECRYPT ? v : o;
         } else {
           const u32x4 p = load_partial(in_rec + 16u * j, rem);
@@ -242,17 +264,22 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
     const uint32_t Lu = (uint32_t)L;
     // PF input buffers: slot u's block is reloaded with slot u+PF*L's as soon as u is consumed,
     // so each load has PF-1 slots of AES in front of its use and no register copies.
+    const int32_t u0 = (int32_t)q - (int32_t)phi;  // negative: the lane sits out step 0
     u32x4 v[PF];
 #pragma unroll
-    for (int d = 0; d < PF; ++d) v[d] = prefetch(q + (uint32_t)d * Lu);
+    for (int d = 0; d < PF; ++d) {
+      const int32_t uu = u0 + d * L;
+      v[d] = prefetch(uu < 0 ? 0u : (uint32_t)uu);
+    }
     uint32_t it = 0;
-    for (uint32_t u = q; u < nslots; u += (uint32_t)PF * Lu) {
-      if (a.sched & 1u) rotate_prio(it++);
+    for (int32_t u = u0; u < (int32_t)nslots; u += PF * L) {
+      if ((a.sched & 1u) && !(a.sched & 4096u)) rotate_prio(it++);
 #pragma unroll
       for (int d = 0; d < PF; ++d) {
-        const uint32_t uu = u + (uint32_t)d * Lu;
-        if (d == 0 || uu < nslots) consume(uu, keystream(uu), v[d]);
-        v[d] = prefetch(uu + (uint32_t)PF * Lu);
+        const int32_t uu = u + d * L;
+        if (a.sched & 4096u) rotate_prio(it++);  // per slot: finer interleaving of equal-work waves
+        if (uu >= 0 && uu < (int32_t)nslots) consume((uint32_t)uu, keystream((uint32_t)uu), v[d]);
+        v[d] = prefetch((uint32_t)(uu + PF * L));
       }
     }
 
@@ -262,8 +289,8 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       f = gmul_byte(acc, gl);  // L = 1: byte table holds H, w = 1
     } else {
       f = u32x4{0u, 0u, 0u, 0u};
-      if (q < nxs) {
-        const uint32_t ulast = q + (uint32_t)L * ((nxs - 1u - q) / (uint32_t)L);
+      if (qs < nxs) {
+        const uint32_t ulast = qs + (uint32_t)L * ((nxs - 1u - qs) / (uint32_t)L);
         const uint32_t w = nxs - ulast;  // 1..L
         f = gmul_nib(acc, kGcmNib + (w - 1u) * 8192u);
       }
@@ -274,12 +301,20 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
 
     if (a.nseg > 1) {
       if (q == 0) a.partial[g] = f;
-      if (s == 0 && (nxs % (uint32_t)L) == q) a.ekj0[r] = ekj0;  // lane that owned slot nxs
+      if (s == 0 && (nxs % (uint32_t)L) == qs) a.ekj0[r] = ekj0;  // lane that owned slot nxs
       continue;
     }
     // single-segment record: finish the tag here
     if (!DECRYPT) {
-      if (q == 0) {
+      if (defer) {  // the tag's window in one store instruction: held data blocks + the tag
+        uint8_t* at = pend_at;
+        u32x4 val = pend;
+        if (qs == (tslot & (uint32_t)(L - 1))) {
+          at = out_rec + a.len;
+          val = f;
+        }
+        if (at) st_blk(at, val);
+      } else if (q == 0) {
         uint8_t* tp = out_rec + a.len;
         st_blk(tp, f);
       }
@@ -303,6 +338,11 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
         }
       }
     }
+  }
+  if (a.probe) {
+    // per-wave end times (lane 0 of each wave): slot 2 + wave index, up to 6 waves sampled
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0u && w < 6u) a.probe[blockIdx.x * 8u + 2u + w] = wall_clock64();
   }
 }
 

@@ -238,6 +238,37 @@ def test_flow_kernel_forms(threads, flags, n, nrec, steps):
     assert np.array_equal(gpu_seal(ctx, nonces, pt), oracle.gcm_seal_batch(key2, nonces, pt))
 
 
+@pytest.mark.parametrize("n", [0, 15, 16, 1000, 1024, 4096, 4097])
+@pytest.mark.parametrize("plan", [(4, 1), (2, 1), (4, 3), (1, 1)])
+@pytest.mark.parametrize("stride_pad", [0, 28])
+def test_output_aligned_windows(n, plan, stride_pad):
+    """Lane kernel with output-aligned windows (cmpi_debug_set_sched bit 13): lanes of a record
+    start phase-shifted so each step's stores fill whole 16L-byte sectors, and a seal holds the
+    tag window's data blocks back to store them with the tag.  Bit-exact seal (dense and wire
+    strides, where every record has its own phase), open, forged record zero-filled."""
+    L = aead.N.lib()
+    L.cmpi_debug_set_sched(7 | 8192)
+    try:
+        aead.force_plan(*plan)
+        nrec = 37
+        pt = records(0x6600 + n, nrec, n)
+        nonces = random_nonces(0x6700 + n, nrec)
+        ctx = aead.AeadCtx(KEY)
+        want = oracle.gcm_seal_batch(KEY, nonces, pt)
+        stride = n + 16 + stride_pad
+        out = empty(nrec * stride, fill=0xAA)
+        ctx.seal_batch(out, dev(pt), dev(nonces), n, nrec, out_stride=stride)
+        got = host(out)[: nrec * stride].reshape(nrec, stride)
+        assert np.array_equal(got[:, : n + 16], want) and (got[:, n + 16:] == 0xAA).all()
+        forged = want.copy()
+        forged[5, n // 2 if n else n + 3] ^= 1
+        back, st = gpu_open(ctx, nonces, forged)
+        assert st[5] == 0 and not back[5].any() and (np.delete(st, 5) == 1).all()
+        assert np.array_equal(np.delete(back, 5, axis=0), np.delete(pt, 5, axis=0))
+    finally:
+        L.cmpi_debug_set_sched(7)
+
+
 @pytest.mark.parametrize("nrec,segments", [(3, 0), (2, 700), (1, 2)])
 def test_lane_groups_many_segments(nrec, segments):
     """1 MiB records on the lane-group plan (wide disabled): hundreds of segment partials per

@@ -18,6 +18,10 @@ ap.add_argument("--seal-only", action="store_true")
 ap.add_argument("--out-stride", type=int, default=0,
                 help="gcm1k seal-only traffic calibration: output record stride (0 = dense n+16)")
 a = ap.parse_args()
+if os.environ.get("SCHED"):  # cmpi_debug_set_sched bits for the profiled run
+    from cryptmpi_2022_amd import _native as _N
+
+    _N.lib().cmpi_debug_set_sched(int(os.environ["SCHED"]))
 if a.out_stride:  # 65 536 x 1 KiB seals into records `out_stride` bytes apart (aligned vs dense)
     from cryptmpi_2022_amd import aead
 
