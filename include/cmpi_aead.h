@@ -5,7 +5,8 @@
  * hot path.  Plain pointers and sizes only; `stream` is a hipStream_t
  * passed as void* (NULL = the legacy default stream).  Device-resident entry points take
  * DEVICE pointers and are asynchronous on `stream`; the *_host entry points take HOST
- * pointers (pinned for full PCIe rate), stage through the device and are synchronous.
+ * pointers (pinned for full PCIe rate) and are synchronous (include/cmpi_async.h: the
+ * non-blocking begin / wait form).
  *
  * Reference interfaces each entry point replaces (file:line):
  *   cmpi_ctx_new(CMPI_AES_128_GCM,…)  EVP_AEAD_CTX_new(EVP_aead_aes_128_gcm(), key, 16, 0)
@@ -123,9 +124,11 @@ int cmpi_gcm_open_batch(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, co
                         size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
                         size_t nrec, int32_t *status, void *workspace, void *stream);
 
-/* Host-memory variants: H2D (hipMemcpyAsync) -> kernel -> D2H on an internal stream, then
- * synchronise.  Returns CMPI_OK, CMPI_EAUTH (open: some record failed; status[] on the host
- * says which, may be NULL) or another error. */
+/* Host-memory variants, synchronous.  Up to 2 MiB of input + output records the kernel reads
+ * and writes page-locked buffers directly (pageable ones through a pinned bounce buffer);
+ * larger calls pipeline H2D -> kernel -> D2H in chunks over internal streams.  Returns CMPI_OK,
+ * CMPI_EAUTH (open: some record failed; status[] on the host says which, may be NULL) or another
+ * error.  Records of length 0 may pass NULL data pointers. */
 int cmpi_gcm_seal_host(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
                        size_t in_stride, const uint8_t *nonces, size_t nonce_stride, size_t len,
                        size_t nrec);

@@ -4,17 +4,18 @@
  * MPI_Waitall complete it, decrypting received messages (MV/src/mpi/pt2pt/isend.c:187-1260,
  * wait.c:244-1780, waitall.c:438-2389; 64 requests in nonblock_req_handler[], isend.c:310-321).
  *
- *   *_host_begin   enqueue H2D -> seal/open kernel -> D2H of a host-memory batch (the record
- *                  layout and status semantics of the synchronous *_host calls, cmpi_aead.h) on
- *                  a pooled stream and return at once with a request;
+ *   *_host_begin   enqueue the seal/open of a host-memory batch (the record layout and status
+ *                  semantics of the synchronous *_host calls, cmpi_aead.h) on a pooled stream
+ *                  and return at once with a request: up to 2 MiB of records the kernel reads
+ *                  and writes page-locked buffers itself, larger ones go H2D -> kernel -> D2H;
  *   cmpi_test      MPI_Test: *done = 1 and the request completed (and freed) when it finished;
  *   cmpi_wait      MPI_Wait: block until done; returns CMPI_OK, CMPI_EAUTH (open: a record
  *                  failed, status[] says which, its plaintext zero-filled) or another error;
  *   cmpi_waitall   MPI_Waitall over n requests (NULL entries skipped, every entry cleared).
  *
- * Input buffers may be reused when *_begin returns (pageable inputs are packed into pinned
- * staging inside it; pinned ones are read by DMA later — keep those until completion, as MPI
- * does).  Output and status buffers must stay valid until the request completes.  Requests are
+ * Input buffers may be reused when *_begin returns if pageable (they are packed into pinned
+ * staging inside it); page-locked ones are read later by DMA or by the kernel — keep those
+ * until completion, as MPI does.  Output and status buffers must stay valid until the request completes.  Requests are
  * independent: any number may be outstanding on one context, from any thread.
  */
 #ifndef CMPI_ASYNC_H
