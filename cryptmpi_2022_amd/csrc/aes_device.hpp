@@ -188,27 +188,6 @@ __device__ __forceinline__ void aes128_enc_ctr(const RoundKeys& k, const RowLane
   enc_last(L, s0, s1, s2, s3, k.w[40], k.w[41], k.w[42], k.w[43]);
 }
 
-// Two counter blocks at once (caches ca / cb), rounds interleaved: twice the independent LDS
-// lookups in flight per wave where few waves share a SIMD (gcm_flow_kernel at 512 threads).
-__device__ __forceinline__ void aes128_enc_ctr2(const RoundKeys& k, const RowLanes& L, const CtrCache& ca,
-                                                uint32_t w3a, const CtrCache& cb, uint32_t w3b, u32x4& oa, u32x4& ob) {
-  const uint32_t ra0 = ca.k0 ^ rotl16(lds32(ra<3>(w3a ^ k.w[3], L.l1)));
-  const uint32_t rb0 = cb.k0 ^ rotl16(lds32(ra<3>(w3b ^ k.w[3], L.l1)));
-  uint32_t a0 = ca.q0 ^ lds32(ra<0>(ra0, L.l0)), a3 = ca.q3 ^ lds32(ra<1>(ra0, L.l1));
-  uint32_t a2 = ca.q2 ^ rotl16(lds32(ra<2>(ra0, L.l0))), a1 = ca.q1 ^ rotl16(lds32(ra<3>(ra0, L.l1)));
-  uint32_t b0 = cb.q0 ^ lds32(ra<0>(rb0, L.l0)), b3 = cb.q3 ^ lds32(ra<1>(rb0, L.l1));
-  uint32_t b2 = cb.q2 ^ rotl16(lds32(ra<2>(rb0, L.l0))), b1 = cb.q1 ^ rotl16(lds32(ra<3>(rb0, L.l1)));
-#pragma unroll
-  for (int r = 3; r < 10; ++r) {
-    enc_round(L, a0, a1, a2, a3, k.w[4 * r], k.w[4 * r + 1], k.w[4 * r + 2], k.w[4 * r + 3]);
-    enc_round(L, b0, b1, b2, b3, k.w[4 * r], k.w[4 * r + 1], k.w[4 * r + 2], k.w[4 * r + 3]);
-  }
-  enc_last(L, a0, a1, a2, a3, k.w[40], k.w[41], k.w[42], k.w[43]);
-  enc_last(L, b0, b1, b2, b3, k.w[40], k.w[41], k.w[42], k.w[43]);
-  oa = u32x4{a0, a1, a2, a3};
-  ob = u32x4{b0, b1, b2, b3};
-}
-
 // AES-128 decryption (FIPS-197 §5.3.5 equivalent inverse cipher) with the Td0/Td1 row image
 // (lanes LD) and the inverse S-box image at lbs = sbase | (lane&31)*4 for the last round.
 __device__ __forceinline__ uint32_t sb0(uint32_t w) { return (w << 7) & 0x7f80u; }

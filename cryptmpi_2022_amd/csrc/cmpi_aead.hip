@@ -254,7 +254,7 @@ std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4
 std::atomic<int> g_wide_chw{1};       // wide plan, host-keyed: barrier-free FLOW kernel with chunk weights (1) or weights in the combine (0)
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
 std::atomic<int> g_flow_nt{1024};     // FLOW wide kernel threads per workgroup (512 / 1024), 0 = round-1 kernel
-std::atomic<int> g_flow_fused{0};     // FLOW wide kernel flags: bit 0 combine fused, bits 1-3 timing ablations, bit 4 round-2-first form, bit 5 no automatic 512-thread workgroups, bit 6 two AES chains per lane (512 threads)
+std::atomic<int> g_flow_fused{0};     // FLOW wide kernel flags: bit 0 combine fused, bits 1-3 timing ablations, bit 4 round-2-first form, bit 5 no automatic 512-thread workgroups
 std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
 std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics: wide-kernel phase timestamps
@@ -552,8 +552,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
       a.sched |= (uint32_t)((flags >> 7) & 3) << 11;  // bits 7-8: no stores / no loads (ablations)
       a.wtab = r4 ? reinterpret_cast<const u32x4*>(c->dt->fnib[0]) : a.wtab;
       const void* fn;
-      if (r4) fn = NT == 512 ? ((flags & 64) ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, true, true>)
-                                             : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, true>))
+      if (r4) fn = NT == 512 ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, true>)
                              : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, true>);
       else fn = NT == 512 ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, false>)
                           : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, false>);

@@ -629,7 +629,7 @@ __device__ __forceinline__ u32x4 flow_tree_r4(u32x4 acc, uint32_t lane) {
   return x;
 }
 
-template <bool DECRYPT, int NT, bool R4, bool ILP2 = false>
+template <bool DECRYPT, int NT, bool R4>
 __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
   const bool prb = a.probe && threadIdx.x == 0u;
   if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
@@ -684,8 +684,8 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       uint32_t n0, n1, n2;
       gcm_nonce(a, r, !DECRYPT && i == 0u && lane == 0u, n0, n1, n2);
       auto prefetch = [&](uint32_t k) -> u32x4 { return load_x(in_rec, base, k); };
-      CtrCache cc, cc2;
-      uint32_t cc_win = 0xffffffffu, cc2_win = 0xffffffffu;
+      CtrCache cc;
+      uint32_t cc_win = 0xffffffffu;
       auto keystream = [&](uint32_t ctr) -> u32x4 {
         const uint32_t w3 = __builtin_bswap32(ctr);
         if (a.sched & 1024u) return u32x4{w3, n0, n1, n2};  // timing ablation: no AES
@@ -696,27 +696,6 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
         uint32_t s0, s1, s2, s3;
         aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
         return u32x4{s0, s1, s2, s3};
-      };
-      // steps k and k+1 together (ILP2): counters 64 apart, each with a window cache of its own
-      // (copied from the other when both sit in one 256-counter window)
-      auto keystream2 = [&](uint32_t ca, uint32_t cb, u32x4& ka, u32x4& kb) {
-        const uint32_t w3a = __builtin_bswap32(ca), w3b = __builtin_bswap32(cb);
-        if (a.sched & 1024u) {
-          ka = u32x4{w3a, n0, n1, n2};
-          kb = u32x4{w3b, n0, n1, n2};
-          return;
-        }
-        if ((ca >> 8) != cc_win) {
-          if ((ca >> 8) == cc2_win) cc = cc2;
-          else ctr_cache_fill(rk, rl, n0, n1, n2, w3a, cc);
-          cc_win = ca >> 8;
-        }
-        if ((cb >> 8) != cc2_win) {
-          if ((cb >> 8) == cc_win) cc2 = cc;
-          else ctr_cache_fill(rk, rl, n0, n1, n2, w3b, cc2);
-          cc2_win = cb >> 8;
-        }
-        aes128_enc_ctr2(rk, rl, cc, w3a, cc2, w3b, ka, kb);
       };
       u32x4 acc = {0u, 0u, 0u, 0u};
       auto consume_ks = [&](uint32_t k, u32x4 v, u32x4 ks) {
@@ -750,19 +729,10 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       uint32_t it = 0;
       for (uint32_t k = 0; k < steps; k += 2u) {
         if (a.sched & 1u) rotate_prio(it++);
-        if (ILP2 && k + 1u < steps) {
-          u32x4 ka, kb;
-          keystream2(ctr_of(k), ctr_of(k + 1u), ka, kb);
-          consume_ks(k, va, ka);
-          va = prefetch(k + 2u);
-          consume_ks(k + 1u, vb, kb);
-          vb = prefetch(k + 3u);
-        } else {
-          consume_ks(k, va, keystream(ctr_of(k)));
-          va = prefetch(k + 2u);
-          if (k + 1u < steps) consume_ks(k + 1u, vb, keystream(ctr_of(k + 1u)));
-          vb = prefetch(k + 3u);
-        }
+        consume_ks(k, va, keystream(ctr_of(k)));
+        va = prefetch(k + 2u);
+        if (k + 1u < steps) consume_ks(k + 1u, vb, keystream(ctr_of(k + 1u)));
+        vb = prefetch(k + 3u);
       }
       u32x4 ekj = {0u, 0u, 0u, 0u};
       if (i == 0u) ekj = keystream(1u);  // E_K(J0) folded into chunk 0's partial

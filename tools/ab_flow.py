@@ -19,8 +19,7 @@ from cryptmpi_2022_amd import aead  # noqa: E402
 
 SHAPES = {"a2a_8x1m": (1 << 20, 8), "64x1m": (1 << 20, 64), "1x64k": (65536, 1)}
 VARIANTS = [("r1", 0, 1), ("flow1024_unfused", 1024, 0), ("flow1024", 1024, 1), ("flow512", 512, 1),
-            ("w4_1024_unfused", 1024, 16), ("w4_1024", 1024, 17), ("fixed1024", 1024, 32), ("fixed512", 512, 32),
-            ("ilp2", 1024, 64)]
+            ("w4_1024_unfused", 1024, 16), ("w4_1024", 1024, 17), ("fixed1024", 1024, 32), ("fixed512", 512, 32)]
 # timing ablations (output wrong, not verified), fused: skip tree (2), chunk-weight product (4), AES (8)
 VARIANTS += [(f"abl{c}", 1024, c | 1) for c in (2, 4, 6, 8, 14)]
 # unfused ablations incl. no stores (128) / no loads (256)
