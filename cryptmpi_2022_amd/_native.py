@@ -110,6 +110,7 @@ _SIGS = {
     "cmpi_debug_force_plan": ([_I, _U32], None),
     "cmpi_debug_force_wide": ([_I, _U32], None),
     "cmpi_debug_set_gcm_prefetch": ([_I], None),
+    "cmpi_debug_set_gcm_form": ([_I], None),
     "cmpi_debug_set_wide_chw": ([_I], None),
     "cmpi_debug_set_flow": ([_I, _I], None),
     "cmpi_debug_set_host_direct": ([_S], None),

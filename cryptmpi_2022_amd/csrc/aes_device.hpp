@@ -455,6 +455,26 @@ __device__ __forceinline__ void rotate_prio(uint32_t t) {
   }
 }
 
+// Progress-based priority: every wave adds one to a workgroup counter in LDS per unit of work it
+// starts and takes priority 3..0 by how far it is behind / ahead of the workgroup average (the
+// counter holds the sum of all waves' progress).  Waves of equal work then finish together
+// instead of spread by issue arbitration (tools/probe/lds_probe.hip, 4 waves/SIMD: 2.71 -> 2.48
+// CU-ns per block against rotate_prio, wave lifetimes 288K..375K -> 347K..362K cycles).
+__device__ __forceinline__ void progress_prio(uint32_t cnt_off, uint32_t done) {
+  uint32_t tot = 0;
+  if ((threadIdx.x & 63u) == 0u)
+    tot = __hip_atomic_fetch_add((lds_u32*)(size_t)cnt_off, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  tot = __builtin_amdgcn_readfirstlane(tot) + 1u;
+  const uint32_t nw = blockDim.x >> 6, mine = done * nw;
+  const uint32_t p = mine + nw <= tot ? 3u : (mine <= tot ? 2u : (mine <= tot + nw ? 1u : 0u));
+  switch (p) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+}
+
 __device__ __forceinline__ u32x4 shfl_down4(u32x4 v, uint32_t d) {
   u32x4 r;
   r[0] = __shfl_down((int)v[0], d);

@@ -251,6 +251,7 @@ std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
 std::atomic<int> g_gcm_mem{0};        // lane kernel record-data cache policy: bit 0 nt loads, bit 1 nt stores
 std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4/6
+std::atomic<int> g_gcm_form{0};       // GCM lane plan: 0 gcm_lane_kernel, 1 the first form gcm_batch_kernel
 std::atomic<int> g_wide_chw{1};       // wide plan, host-keyed: barrier-free FLOW kernel with chunk weights (1) or weights in the combine (0)
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
 std::atomic<int> g_flow_nt{1024};     // FLOW wide kernel threads per workgroup (512 / 1024), 0 = round-1 kernel
@@ -258,7 +259,7 @@ std::atomic<int> g_flow_fused{0};     // FLOW wide kernel flags: bit 0 combine f
 std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
 std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics: wide-kernel phase timestamps
-std::atomic<int> g_sched{7};         // wave-priority rotation: bit 0 GCM, bit 1 CTR, bit 2 OCB
+std::atomic<int> g_sched{7 | 16384};  // wave priority: bit 0 GCM, bit 1 CTR, bit 2 OCB rotation; bit 14 GCM progress-based
 std::atomic<int> g_gcm_ablation{0};  // timing ablation of the L=4 seal kernel (tools/ablate.py)  // LDS requested by the CTR kernel (occupancy experiments)
 
 GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
@@ -435,7 +436,18 @@ int launch_gcm_combine(const cmpi_ctx* c, cmpi::dev::GcmCombineArgs& ca, uint32_
 
 template <int L, bool DEC>
 int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
-  auto fn = cmpi::dev::gcm_batch_kernel<L, DEC>;
+  // default: the round-2 lane kernel; the first form stays behind the A/B / ablation knobs
+  const bool first_form = g_gcm_form.load() == 1 || g_gcm_pf.load() != 2 || g_gcm_mem.load() != 0 ||
+                          (!DEC && g_gcm_ablation.load() != 0 && g_gcm_ablation.load() < 16) || (a.sched & 8192u);
+  auto fn = first_form ? cmpi::dev::gcm_batch_kernel<L, DEC> : cmpi::dev::gcm_lane_kernel<L, DEC>;
+  if constexpr (!DEC) {  // ablations of the round-2 form (tools/ablate_split.py): 16 no memory, 32 no AES
+    switch (g_gcm_ablation.load()) {
+      case 16: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 2, 1>; break;
+      case 32: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 2, 2>; break;
+      case 48: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 2, 3>; break;
+      default: break;
+    }
+  }
   switch (g_gcm_pf.load()) {
     case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 3>; break;
     case 4: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 4>; break;
@@ -1290,9 +1302,9 @@ int cmpi_host_unregister(void* ptr) {
   return CMPI_OK;
 }
 
-void cmpi_debug_set_sched(int mode) { g_sched.store(mode & (7 | 4096 | 8192)); }
+void cmpi_debug_set_sched(int mode) { g_sched.store(mode & (7 | 4096 | 8192 | 16384)); }
 void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)16 << 20)); }
-void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 15); }
+void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 63); }
 
 void cmpi_debug_set_ctr_lds(int lds_bytes) {
   g_ctr_lds.store(lds_bytes >= 65536 && lds_bytes <= 163840 ? lds_bytes : 65536);
@@ -1334,6 +1346,7 @@ void cmpi_debug_event_free(void* ev) {
 }
 void cmpi_debug_set_wide_probe(void* buf) { g_wide_probe.store(reinterpret_cast<uint64_t*>(buf)); }
 
+void cmpi_debug_set_gcm_form(int form) { g_gcm_form.store(form == 1 ? 1 : 0); }
 void cmpi_debug_set_gcm_prefetch(int slots) { g_gcm_pf.store(slots == 3 || slots == 4 || slots == 6 ? slots : 2); }
 
 void cmpi_debug_force_wide(int mode, uint32_t steps) {

@@ -134,10 +134,12 @@ __device__ __forceinline__ void gcm_nonce(const GcmArgs& a, uint32_t r, bool wri
 }
 
 // LDS: GHASH byte table [v][p] @0 (64 KiB), AES row image @64K (64 KiB), nibble tables of
-// H^1..H^L @128K (L x 8 KiB, L > 1).  L = 4 uses the whole 160 KiB of the CU.
+// H^1..H^(L-1) @128K ((L-1) x 8 KiB; a lane whose weight is H^L multiplies by the byte table),
+// then the workgroup's progress counter (16 B, gcm_progress_prio).
 constexpr uint32_t kGcmRows = 65536u;
 constexpr uint32_t kGcmNib = 131072u;
-__host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return kGcmNib + (L > 1 ? (uint32_t)L * 8192u : 0u); }
+__host__ __device__ constexpr uint32_t gcm_prog_off(int L) { return kGcmNib + (uint32_t)(L - 1) * 8192u; }
+__host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return gcm_prog_off(L) + 16u; }
 
 // ABL (timing ablation, wrong results): bit 0 = GHASH multiply skipped, bit 1 = AES skipped
 // (keystream = counter block), bit 2 = record data addressed as one coalesced stream per wave
@@ -148,7 +150,8 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
   stage_copy(a.htab, 0u, 4096u);
   stage_rows(a.te0, kGcmRows);
-  if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)L * 512u);
+  if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)(L - 1) * 512u);
+  if (threadIdx.x == 0u) lds_st32(gcm_prog_off(L), 0u);
   __syncthreads();
   if (prb) a.probe[blockIdx.x * 8u + 1u] = wall_clock64();
   if (ABL & 8) {  // prologue only (table staging cost)
@@ -168,6 +171,7 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
 
   const uint32_t groups_per_iter = (gridDim.x * blockDim.x) / (uint32_t)L;
+  uint32_t done = 0;  // slots this wave has started (progress_prio)
   for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / (uint32_t)L; g < a.ngroups; g += groups_per_iter) {
     const uint32_t r = (a.nseg == 1) ? g : g / a.nseg;
     const uint32_t s = g - r * a.nseg;
@@ -261,7 +265,6 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       if (!(ABL & 2)) aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
       return u32x4{s0, s1, s2, s3};
     };
-    const uint32_t Lu = (uint32_t)L;
     // PF input buffers: slot u's block is reloaded with slot u+PF*L's as soon as u is consumed,
     // so each load has PF-1 slots of AES in front of its use and no register copies.
     const int32_t u0 = (int32_t)q - (int32_t)phi;  // negative: the lane sits out step 0
@@ -272,12 +275,14 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       v[d] = prefetch(uu < 0 ? 0u : (uint32_t)uu);
     }
     uint32_t it = 0;
+    const uint32_t prio_mode = a.sched & (1u | 4096u | 16384u);
     for (int32_t u = u0; u < (int32_t)nslots; u += PF * L) {
-      if ((a.sched & 1u) && !(a.sched & 4096u)) rotate_prio(it++);
+      if (prio_mode == 1u) rotate_prio(it++);
 #pragma unroll
       for (int d = 0; d < PF; ++d) {
         const int32_t uu = u + d * L;
-        if (a.sched & 4096u) rotate_prio(it++);  // per slot: finer interleaving of equal-work waves
+        if (prio_mode & 16384u) progress_prio(gcm_prog_off(L), ++done);  // behind the workgroup -> first
+        else if (prio_mode & 4096u) rotate_prio(it++);  // per slot: finer interleaving of equal-work waves
         if (uu >= 0 && uu < (int32_t)nslots) consume((uint32_t)uu, keystream((uint32_t)uu), v[d]);
         v[d] = prefetch((uint32_t)(uu + PF * L));
       }
@@ -291,8 +296,9 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
       f = u32x4{0u, 0u, 0u, 0u};
       if (qs < nxs) {
         const uint32_t ulast = qs + (uint32_t)L * ((nxs - 1u - qs) / (uint32_t)L);
-        const uint32_t w = nxs - ulast;  // 1..L
-        f = gmul_nib(acc, kGcmNib + (w - 1u) * 8192u);
+        const uint32_t w = nxs - ulast;  // 1..L: H^L is the Horner byte table, H^1..H^(L-1) nibble tables
+        if (w == (uint32_t)L) f = gmul_byte(acc, gl);
+        else f = gmul_nib(acc, kGcmNib + (w - 1u) * 8192u);
       }
     }
     if (a.nseg == 1) f ^= ekj0;
@@ -341,6 +347,177 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
   }
   if (a.probe) {
     // per-wave end times (lane 0 of each wave): slot 2 + wave index, up to 6 waves sampled
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0u && w < 6u) a.probe[blockIdx.x * 8u + 2u + w] = wall_clock64();
+  }
+}
+
+// Lane-group kernel, round-2 form (the default lane plan): the same decomposition and LDS
+// layout as gcm_batch_kernel, but a segment's slots are split into
+//   * the FULL data blocks [0, nfull): a branch-free main loop — keystream, XOR with the block
+//     prefetched PF slots ahead, 16-B store, Horner step — with no partial-block path, no J0 or
+//     length-block case and no held-back stores inside, so the waitcnt pass sees one load, one
+//     store and LDS traffic per slot and waits only for the load a slot consumes (the first form
+//     also waited, through its conditional store / partial-block paths, for the load issued one
+//     slot earlier and for the previous store, and carried ~70 SGPR-spill lane moves and ~90
+//     register copies per two slots);
+//   * the <= 3 special slots at the segment's end (a partial last block, the length block, the
+//     E_K(J0) slot of segment 0): a tail step, AES only where one is needed.
+// Every segment's special slots are its last ones, so Horner order is unchanged.
+// ABL (timing ablation, wrong results): bit 0 = main-loop record loads/stores skipped (the
+// keystream is folded into the Horner input instead), bit 1 = AES skipped (keystream = counter).
+template <int L, bool DECRYPT, int PF = 2, int ABL = 0>
+__global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
+  const bool prb = a.probe && threadIdx.x == 0u;
+  if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
+  stage_copy(a.htab, 0u, 4096u);
+  stage_rows(a.te0, kGcmRows);
+  if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)(L - 1) * 512u);
+  if (threadIdx.x == 0u) lds_st32(gcm_prog_off(L), 0u);
+  __syncthreads();
+  if (prb) a.probe[blockIdx.x * 8u + 1u] = wall_clock64();
+
+  const RoundKeys rk = load_round_keys(a.rk, a.rkp);  // folded (host / keysetup kernel)
+  const uint32_t lane = threadIdx.x & 63u;
+  const RowLanes rl = row_lanes(kGcmRows);
+  const GhashLane gl = ghash_lane();
+  const uint32_t q = threadIdx.x & (uint32_t)(L - 1);
+  const uint32_t nb = a.nb;
+  const uint32_t rem = a.len - 16u * (nb ? nb - 1u : 0u);       // bytes in the last data block
+  const uint32_t nbf = nb == 0u ? 0u : (rem == 16u ? nb : nb - 1u);  // full data blocks
+  const uint64_t cbits = (uint64_t)a.len * 8u;
+  const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
+  const bool pprio = (a.sched & 16384u) != 0u;
+  const bool rprio = !pprio && (a.sched & 1u) != 0u;
+
+  uint32_t done = 0;  // slots this wave has started (progress_prio)
+  const uint32_t groups_per_iter = (gridDim.x * blockDim.x) / (uint32_t)L;
+  for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / (uint32_t)L; g < a.ngroups; g += groups_per_iter) {
+    const uint32_t r = (a.nseg == 1) ? g : g / a.nseg;
+    const uint32_t s = g - r * a.nseg;
+    const uint32_t x0 = (s == 0) ? 0u : a.r0 + (s - 1u) * a.G;
+    const uint32_t x1 = a.r0 + s * a.G;
+    const uint32_t nxs = x1 - x0;                      // X-blocks in this segment
+    const uint32_t nslots = nxs + (s == 0 ? 1u : 0u);  // + the J0 slot
+    const uint32_t xf = x1 < nbf ? x1 : nbf;
+    const uint32_t nfull = xf > x0 ? xf - x0 : 0u;     // full data-block slots [0, nfull)
+    const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
+    uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
+    uint32_t n0, n1, n2;
+    gcm_nonce(a, r, !DECRYPT && s == 0u && q == 0u, n0, n1, n2);
+
+    CtrCache cc;
+    uint32_t cc_win = 0xffffffffu;
+    auto keystream = [&](uint32_t ctr) -> u32x4 {  // E_K(nonce || ctr)
+      const uint32_t w3 = __builtin_bswap32(ctr);
+      if ((ctr >> 8) != cc_win) {
+        ctr_cache_fill(rk, rl, n0, n1, n2, w3, cc);
+        cc_win = ctr >> 8;
+      }
+      uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = w3;
+      if (!(ABL & 2)) aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
+      return u32x4{s0, s1, s2, s3};
+    };
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    u32x4 ekj0 = {0u, 0u, 0u, 0u};
+
+    // ---- full data blocks: slot u = X position x0 + u, counter 2 + x0 + u
+    const uint8_t* ip = in_rec + 16u * x0;
+    uint8_t* op = out_rec + 16u * x0;
+    auto full = [&](uint32_t u, u32x4 v) {
+      if (pprio) progress_prio(gcm_prog_off(L), ++done);
+      else if (rprio) rotate_prio(done++);
+      const u32x4 o = v ^ keystream(2u + x0 + u);
+      if (!(ABL & 1)) st_blk(op + 16u * u, o);
+      acc = gmul_byte(acc, gl) ^ (DECRYPT ? v : o);
+    };
+    uint32_t u = q;
+    if (nfull > 0u) {
+      // PF input buffers: slot u's block is reloaded with slot u + PF*L's once u is consumed;
+      // loads past the full blocks are clamped to the segment's first block (value unused)
+      auto ld = [&](uint32_t uu) {
+        if (ABL & 1) return u32x4{uu, x0, lane, 0u};
+        return ld_blk(ip + 16u * (uu < nfull ? uu : 0u));
+      };
+      u32x4 v[PF];
+#pragma unroll
+      for (int d = 0; d < PF; ++d) v[d] = ld(u + (uint32_t)(d * L));
+      for (; u + (uint32_t)((PF - 1) * L) < nfull; u += (uint32_t)(PF * L)) {
+#pragma unroll
+        for (int d = 0; d < PF; ++d) {
+          const uint32_t uu = u + (uint32_t)(d * L);
+          full(uu, v[d]);
+          v[d] = ld(uu + (uint32_t)(PF * L));
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < PF - 1; ++d) {
+        const uint32_t uu = u + (uint32_t)(d * L);
+        if (uu < nfull) full(uu, v[d]);
+      }
+    }
+    // ---- special slots: partial last block, length block, J0 (the lane's slots >= nfull)
+    for (uint32_t ut = nfull <= q ? q : q + (uint32_t)L * ((nfull - q + (uint32_t)L - 1u) / (uint32_t)L); ut < nslots;
+         ut += (uint32_t)L) {
+      const uint32_t j = x0 + ut;
+      const bool j0 = ut >= nxs;
+      u32x4 ks = {0u, 0u, 0u, 0u};
+      if (j0 || j < nb) ks = keystream(j0 ? 1u : 2u + j);
+      if (j0) {
+        ekj0 = ks;
+        continue;
+      }
+      u32x4 x = lenblk;
+      if (j < nb) {  // the partial last block (rem < 16)
+        const u32x4 p = load_partial(in_rec + 16u * j, rem);
+        const u32x4 o = mask_bytes(p ^ ks, rem);
+        store_partial(out_rec + 16u * j, o, rem);
+        x = DECRYPT ? p : o;
+      }
+      acc = gmul_byte(acc, gl) ^ x;
+    }
+
+    // ---- weight the lane's Horner sum by H^w, w = nxs - (lane's last X slot)
+    u32x4 f = {0u, 0u, 0u, 0u};
+    if (L == 1) {
+      f = gmul_byte(acc, gl);  // L = 1: byte table holds H, w = 1
+    } else if (q < nxs) {
+      const uint32_t ulast = q + (uint32_t)L * ((nxs - 1u - q) / (uint32_t)L);
+      const uint32_t w = nxs - ulast;  // 1..L: H^L is the Horner byte table, H^1..H^(L-1) nibble tables
+      if (w == (uint32_t)L) f = gmul_byte(acc, gl);
+      else f = gmul_nib(acc, kGcmNib + (w - 1u) * 8192u);
+    }
+    if (a.nseg == 1) f ^= ekj0;
+#pragma unroll
+    for (int m = 1; m < L; m <<= 1) f ^= shfl_xor4(f, m);
+
+    if (a.nseg > 1) {
+      if (q == 0) a.partial[g] = f;
+      if (s == 0 && (nxs % (uint32_t)L) == q) a.ekj0[r] = ekj0;  // lane that owned slot nxs
+      continue;
+    }
+    // single-segment record: finish the tag here
+    if (!DECRYPT) {
+      if (q == 0) st_blk(out_rec + a.len, f);
+    } else {
+      int ok = 1;
+      if (q == 0) {
+        const u32x4 d = ld_blk(in_rec + a.len) ^ f;
+        ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+        if (a.status) a.status[r] = ok;
+      }
+      if (L > 1) ok = __shfl(ok, (int)(lane & ~(uint32_t)(L - 1)));
+      if (!ok) {  // zero-fill this record's plaintext (aead.h:276-278)
+        for (uint32_t v = q; v < nxs; v += (uint32_t)L) {
+          const uint32_t j = x0 + v;
+          if (j >= nb) continue;
+          if (j + 1u < nb || rem == 16u) st_blk(out_rec + 16u * j, u32x4{0u, 0u, 0u, 0u});
+          else store_partial(out_rec + 16u * j, u32x4{0u, 0u, 0u, 0u}, rem);
+        }
+      }
+    }
+  }
+  if (a.probe) {
     const uint32_t w = threadIdx.x >> 6;
     if ((threadIdx.x & 63u) == 0u && w < 6u) a.probe[blockIdx.x * 8u + 2u + w] = wall_clock64();
   }

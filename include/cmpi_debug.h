@@ -18,17 +18,23 @@ extern "C" {
  * (0 = automatic) for every subsequent launch in the process. */
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments);
 /* Timing ablation of the GCM seal kernel (results become WRONG): 0 full, 1 no GHASH multiply,
- * 2 no AES, 3 neither, 4 coalesced stand-in addressing, 7 = 3 + 4, 8 = table staging only. */
+ * 2 no AES, 3 neither, 4 coalesced stand-in addressing, 7 = 3 + 4, 8 = table staging only (first form,
+ * gcm_batch_kernel); 16 no record loads/stores, 32 no AES, 48 both (gcm_lane_kernel). */
 void cmpi_debug_set_gcm_ablation(int mode);
 /* CTR kernel occupancy experiment: dynamic LDS bytes requested (65536..163840; more than
  * 80 KiB forces one 1024-thread block per CU). */
 void cmpi_debug_set_ctr_lds(int lds_bytes);
-/* Wave-priority rotation in the main loops (default 7): bit 0 GCM, bit 1 CTR, bit 2 OCB. */
+/* Wave priority in the main loops (default 7 | 16384): bit 0 GCM, bit 1 CTR, bit 2 OCB rotate it per
+ * step; GCM lane kernel: bit 12 rotates per slot, bit 13 output-aligned windows, bit 14
+ * progress-based priority (behind the workgroup average -> higher). */
 void cmpi_debug_set_sched(int mode);
 /* Chunk bytes of the pipelined host path (*_host calls; 0 = default 16 MiB). */
 void cmpi_debug_set_host_chunk(size_t bytes);
 /* GCM lane-group kernel: input prefetch depth in slots (2, 3, 4 or 6; anything else = 2). */
 void cmpi_debug_set_gcm_prefetch(int slots);
+/* GCM lane plan kernel: 0 = gcm_lane_kernel (default), 1 = the first form gcm_batch_kernel (also
+ * selected by a prefetch depth other than 2, the cache-policy and ablation knobs, sched bit 13). */
+void cmpi_debug_set_gcm_form(int form);
 /* Diagnostics: when buf (device, >= 8 x grid u64) is non-null, every gcm_wide_kernel workgroup
    writes wall-clock (100 MHz) timestamps of its phases at buf[8*block + 0..6]: start, tables
    staged, own Horner done, all Horner done, weight tables staged, weights done, end. */

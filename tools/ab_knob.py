@@ -3,6 +3,7 @@
 HIP-event median of seal and open per knob value, one process.
 
     python tools/ab_knob.py cmpi_debug_set_gcm_prefetch 2,3,4,6 gcm1k gcm4k
+    python tools/ab_knob.py cmpi_debug_set_gcm_form,cmpi_debug_set_sched 1:7,0:16391 gcm1k   (several knobs)
 """
 import json
 import os
@@ -14,8 +15,13 @@ import torch  # noqa: E402
 from bench import Workload  # noqa: E402
 from cryptmpi_2022_amd import _native as N  # noqa: E402
 
-setter = getattr(N.lib(), sys.argv[1])
-values = [int(x) for x in sys.argv[2].split(",")]
+_setters = [getattr(N.lib(), n) for n in sys.argv[1].split(",")]
+values = sys.argv[2].split(",")
+
+
+def setter(v):
+    for fn, x in zip(_setters, str(v).split(":")):
+        fn(int(x))
 res = {}
 for wl in sys.argv[3:]:
     w = Workload(wl, 0, seed=3)
