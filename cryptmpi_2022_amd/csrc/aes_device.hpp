@@ -61,8 +61,8 @@ __device__ __forceinline__ uint32_t byte1_mask() {
   return m;
 }
 template <int R>
-__device__ __forceinline__ uint32_t ra(uint32_t s, uint32_t lb) {
-  if constexpr (R == 1) return __builtin_amdgcn_bitop3_b32(s, byte1_mask(), lb, 0xEA);  // (s & m) | lb
+__device__ __forceinline__ uint32_t ra(uint32_t s, uint32_t lb, uint32_t m = 0u) {
+  if constexpr (R == 1) return __builtin_amdgcn_bitop3_b32(s, m, lb, 0xEA);  // (s & m) | lb, m = byte1_mask()
   return perm(s, lb, 0x03020400u | ((uint32_t)R << 8));
 }
 
@@ -84,21 +84,22 @@ __device__ __forceinline__ RoundKeys fold_keys(const RoundKeys& k) {
 }
 
 // Lane constants of a row image at `base` (multiple of 64 KiB): Te0/Td0 half and Te1/Td1 half.
+// m: the byte-1 mask in a VGPR, materialised once per kernel (per use it cost a v_mov per round).
 struct RowLanes {
-  uint32_t l0, l1;
+  uint32_t l0, l1, m;
 };
 __device__ __forceinline__ RowLanes row_lanes(uint32_t base) {
   const uint32_t l = ((threadIdx.x & 31u) << 2) | base;
-  return RowLanes{l, l | 128u};
+  return RowLanes{l, l | 128u, byte1_mask()};
 }
 
 // One AES-128 encryption round (rounds 1..9) on state s, encryption row image; k* folded.
 __device__ __forceinline__ void enc_round(const RowLanes& L, uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
                                           uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  const uint32_t a0 = lds32(ra<0>(s0, L.l0)), a1 = lds32(ra<1>(s1, L.l1)), a2 = lds32(ra<2>(s2, L.l0)), a3 = lds32(ra<3>(s3, L.l1));
-  const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l1)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l1));
-  const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l1)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l1));
-  const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l1)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l1));
+  const uint32_t a0 = lds32(ra<0>(s0, L.l0)), a1 = lds32(ra<1>(s1, L.l1, L.m)), a2 = lds32(ra<2>(s2, L.l0)), a3 = lds32(ra<3>(s3, L.l1));
+  const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l1, L.m)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l1));
+  const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l1, L.m)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l1));
+  const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l1, L.m)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l1));
   s0 = xor3(a0, a1, rotl16(xor3(a2, a3, k0)));
   s1 = xor3(b0, b1, rotl16(xor3(b2, b3, k1)));
   s2 = xor3(c0, c1, rotl16(xor3(c2, c3, k2)));
@@ -108,10 +109,10 @@ __device__ __forceinline__ void enc_round(const RowLanes& L, uint32_t& s0, uint3
 // Last encryption round: S[x] = byte 1 of Te0[x]; gather byte 1 of the four lookups per column.
 __device__ __forceinline__ void enc_last(const RowLanes& L, uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
                                          uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  const uint32_t a0 = lds32(ra<0>(s0, L.l0)), a1 = lds32(ra<1>(s1, L.l0)), a2 = lds32(ra<2>(s2, L.l0)), a3 = lds32(ra<3>(s3, L.l0));
-  const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l0)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l0));
-  const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l0)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l0));
-  const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l0)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l0));
+  const uint32_t a0 = lds32(ra<0>(s0, L.l0)), a1 = lds32(ra<1>(s1, L.l0, L.m)), a2 = lds32(ra<2>(s2, L.l0)), a3 = lds32(ra<3>(s3, L.l0));
+  const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l0, L.m)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l0));
+  const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l0, L.m)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l0));
+  const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l0, L.m)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l0));
   s0 = xor3(perm(a1, a0, 0x0c0c0501u), perm(a3, a2, 0x05010c0cu), k0);
   s1 = xor3(perm(b1, b0, 0x0c0c0501u), perm(b3, b2, 0x05010c0cu), k1);
   s2 = xor3(perm(c1, c0, 0x0c0c0501u), perm(c3, c2, 0x05010c0cu), k2);
@@ -161,16 +162,16 @@ struct CtrCache {
 __device__ __forceinline__ void ctr_cache_fill(const RoundKeys& k, const RowLanes& L, uint32_t w0, uint32_t w1,
                                                uint32_t w2, uint32_t w3, CtrCache& c) {
   const uint32_t t0 = w0 ^ k.w[0], t1 = w1 ^ k.w[1], t2 = w2 ^ k.w[2], t3 = w3 ^ k.w[3];
-  c.k0 = xor3(lds32(ra<0>(t0, L.l0)), lds32(ra<1>(t1, L.l1)), srot16(k.w[4])) ^ rotl16(lds32(ra<2>(t2, L.l0)));
-  const uint32_t r1 = xor3(lds32(ra<0>(t1, L.l0)), lds32(ra<1>(t2, L.l1)), srot16(k.w[5])) ^
+  c.k0 = xor3(lds32(ra<0>(t0, L.l0)), lds32(ra<1>(t1, L.l1, L.m)), srot16(k.w[4])) ^ rotl16(lds32(ra<2>(t2, L.l0)));
+  const uint32_t r1 = xor3(lds32(ra<0>(t1, L.l0)), lds32(ra<1>(t2, L.l1, L.m)), srot16(k.w[5])) ^
                       rotl16(lds32(ra<2>(t3, L.l0)) ^ lds32(ra<3>(t0, L.l1)));
-  const uint32_t r2 = xor3(lds32(ra<0>(t2, L.l0)), lds32(ra<1>(t3, L.l1)), srot16(k.w[6])) ^
+  const uint32_t r2 = xor3(lds32(ra<0>(t2, L.l0)), lds32(ra<1>(t3, L.l1, L.m)), srot16(k.w[6])) ^
                       rotl16(lds32(ra<2>(t0, L.l0)) ^ lds32(ra<3>(t1, L.l1)));
-  const uint32_t r3 = xor3(lds32(ra<0>(t3, L.l0)), lds32(ra<1>(t0, L.l1)), srot16(k.w[7])) ^
+  const uint32_t r3 = xor3(lds32(ra<0>(t3, L.l0)), lds32(ra<1>(t0, L.l1, L.m)), srot16(k.w[7])) ^
                       rotl16(lds32(ra<2>(t1, L.l0)) ^ lds32(ra<3>(t2, L.l1)));
-  c.q0 = xor3(lds32(ra<1>(r1, L.l1)), srot16(k.w[8]), rotl16(lds32(ra<2>(r2, L.l0)) ^ lds32(ra<3>(r3, L.l1))));
-  c.q1 = xor3(lds32(ra<0>(r1, L.l0)), lds32(ra<1>(r2, L.l1)), srot16(k.w[9])) ^ rotl16(lds32(ra<2>(r3, L.l0)));
-  c.q2 = xor3(lds32(ra<0>(r2, L.l0)), lds32(ra<1>(r3, L.l1)), srot16(k.w[10])) ^ rotl16(lds32(ra<3>(r1, L.l1)));
+  c.q0 = xor3(lds32(ra<1>(r1, L.l1, L.m)), srot16(k.w[8]), rotl16(lds32(ra<2>(r2, L.l0)) ^ lds32(ra<3>(r3, L.l1))));
+  c.q1 = xor3(lds32(ra<0>(r1, L.l0)), lds32(ra<1>(r2, L.l1, L.m)), srot16(k.w[9])) ^ rotl16(lds32(ra<2>(r3, L.l0)));
+  c.q2 = xor3(lds32(ra<0>(r2, L.l0)), lds32(ra<1>(r3, L.l1, L.m)), srot16(k.w[10])) ^ rotl16(lds32(ra<3>(r1, L.l1)));
   c.q3 = xor3(lds32(ra<0>(r3, L.l0)), srot16(k.w[11]), rotl16(lds32(ra<2>(r1, L.l0)) ^ lds32(ra<3>(r2, L.l1))));
 }
 
@@ -180,7 +181,7 @@ __device__ __forceinline__ void aes128_enc_ctr(const RoundKeys& k, const RowLane
   const uint32_t t3 = w3 ^ k.w[3];
   const uint32_t r0 = c.k0 ^ rotl16(lds32(ra<3>(t3, L.l1)));
   s0 = c.q0 ^ lds32(ra<0>(r0, L.l0));
-  s3 = c.q3 ^ lds32(ra<1>(r0, L.l1));
+  s3 = c.q3 ^ lds32(ra<1>(r0, L.l1, L.m));
   s2 = c.q2 ^ rotl16(lds32(ra<2>(r0, L.l0)));
   s1 = c.q1 ^ rotl16(lds32(ra<3>(r0, L.l1)));
 #pragma unroll
@@ -205,10 +206,10 @@ __device__ __forceinline__ void aes128_dec(const RoundKeys& k, const RowLanes& L
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
     // InvShiftRows: output column c takes row r from column c - r
-    const uint32_t a0 = lds32(ra<0>(s0, LD.l0)), a1 = lds32(ra<1>(s3, LD.l1)), a2 = lds32(ra<2>(s2, LD.l0)), a3 = lds32(ra<3>(s1, LD.l1));
-    const uint32_t b0 = lds32(ra<0>(s1, LD.l0)), b1 = lds32(ra<1>(s0, LD.l1)), b2 = lds32(ra<2>(s3, LD.l0)), b3 = lds32(ra<3>(s2, LD.l1));
-    const uint32_t c0 = lds32(ra<0>(s2, LD.l0)), c1 = lds32(ra<1>(s1, LD.l1)), c2 = lds32(ra<2>(s0, LD.l0)), c3 = lds32(ra<3>(s3, LD.l1));
-    const uint32_t d0 = lds32(ra<0>(s3, LD.l0)), d1 = lds32(ra<1>(s2, LD.l1)), d2 = lds32(ra<2>(s1, LD.l0)), d3 = lds32(ra<3>(s0, LD.l1));
+    const uint32_t a0 = lds32(ra<0>(s0, LD.l0)), a1 = lds32(ra<1>(s3, LD.l1, LD.m)), a2 = lds32(ra<2>(s2, LD.l0)), a3 = lds32(ra<3>(s1, LD.l1));
+    const uint32_t b0 = lds32(ra<0>(s1, LD.l0)), b1 = lds32(ra<1>(s0, LD.l1, LD.m)), b2 = lds32(ra<2>(s3, LD.l0)), b3 = lds32(ra<3>(s2, LD.l1));
+    const uint32_t c0 = lds32(ra<0>(s2, LD.l0)), c1 = lds32(ra<1>(s1, LD.l1, LD.m)), c2 = lds32(ra<2>(s0, LD.l0)), c3 = lds32(ra<3>(s3, LD.l1));
+    const uint32_t d0 = lds32(ra<0>(s3, LD.l0)), d1 = lds32(ra<1>(s2, LD.l1, LD.m)), d2 = lds32(ra<2>(s1, LD.l0)), d3 = lds32(ra<3>(s0, LD.l1));
     s0 = xor3(a0, a1, rotl16(xor3(a2, a3, k.w[4 * r + 0])));  // k folded
     s1 = xor3(b0, b1, rotl16(xor3(b2, b3, k.w[4 * r + 1])));
     s2 = xor3(c0, c1, rotl16(xor3(c2, c3, k.w[4 * r + 2])));

@@ -442,9 +442,12 @@ int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size
   auto fn = first_form ? cmpi::dev::gcm_batch_kernel<L, DEC> : cmpi::dev::gcm_lane_kernel<L, DEC>;
   if constexpr (!DEC) {  // ablations of the round-2 form (tools/ablate_split.py): 16 no memory, 32 no AES
     switch (g_gcm_ablation.load()) {
-      case 16: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 2, 1>; break;
-      case 32: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 2, 2>; break;
-      case 48: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 2, 3>; break;
+      case 16: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 1>; break;
+      case 32: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 2>; break;
+      case 48: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 3>; break;
+      case 64 + 16: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 5>; break;  // AES only
+      case 64 + 32: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 6>; break;  // memory only
+      case 64: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 4>; break;
       default: break;
     }
   }
@@ -1304,7 +1307,7 @@ int cmpi_host_unregister(void* ptr) {
 
 void cmpi_debug_set_sched(int mode) { g_sched.store(mode & (7 | 4096 | 8192 | 16384)); }
 void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)16 << 20)); }
-void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 63); }
+void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 127); }
 
 void cmpi_debug_set_ctr_lds(int lds_bytes) {
   g_ctr_lds.store(lds_bytes >= 65536 && lds_bytes <= 163840 ? lds_bytes : 65536);

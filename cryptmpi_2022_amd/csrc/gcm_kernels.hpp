@@ -365,8 +365,12 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
 //     E_K(J0) slot of segment 0): a tail step, AES only where one is needed.
 // Every segment's special slots are its last ones, so Horner order is unchanged.
 // ABL (timing ablation, wrong results): bit 0 = main-loop record loads/stores skipped (the
-// keystream is folded into the Horner input instead), bit 1 = AES skipped (keystream = counter).
-template <int L, bool DECRYPT, int PF = 2, int ABL = 0>
+// keystream is folded into the Horner input instead), bit 1 = AES skipped (keystream = counter),
+// bit 2 = main-loop GHASH multiply skipped (the Horner step is an XOR).
+// PF = 1 (one input block in flight per lane, loaded a whole slot ahead) is the default: with PF = 2
+// the kernel needed 128 VGPRs and spilled 19 to scratch (per-record scratch traffic measured as
+// +13 MB reads / +16 MB writes per config-2 launch); at PF = 1 it has 97 VGPRs, no spills.
+template <int L, bool DECRYPT, int PF = 1, int ABL = 0>
 __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
   const bool prb = a.probe && threadIdx.x == 0u;
   if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
@@ -429,15 +433,18 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
       else if (rprio) rotate_prio(done++);
       const u32x4 o = v ^ keystream(2u + x0 + u);
       if (!(ABL & 1)) st_blk(op + 16u * u, o);
-      acc = gmul_byte(acc, gl) ^ (DECRYPT ? v : o);
+      acc = ((ABL & 4) ? acc : gmul_byte(acc, gl)) ^ (DECRYPT ? v : o);
     };
     uint32_t u = q;
     if (nfull > 0u) {
       // PF input buffers: slot u's block is reloaded with slot u + PF*L's once u is consumed;
-      // loads past the full blocks are clamped to the segment's first block (value unused)
+      // loads past the full blocks are clamped to the segment's LAST full block (value unused):
+      // its line was just read, so the clamped load hits L2 (clamped to the first block it
+      // re-read a line fetched ~60 us earlier — +23 MB HBM reads per config-2 launch, and the
+      // extra L2 traffic evicted partially written output lines early: +17 MB writes)
       auto ld = [&](uint32_t uu) {
         if (ABL & 1) return u32x4{uu, x0, lane, 0u};
-        return ld_blk(ip + 16u * (uu < nfull ? uu : 0u));
+        return ld_blk(ip + 16u * (uu < nfull ? uu : nfull - 1u));
       };
       u32x4 v[PF];
 #pragma unroll

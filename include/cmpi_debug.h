@@ -19,7 +19,8 @@ extern "C" {
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments);
 /* Timing ablation of the GCM seal kernel (results become WRONG): 0 full, 1 no GHASH multiply,
  * 2 no AES, 3 neither, 4 coalesced stand-in addressing, 7 = 3 + 4, 8 = table staging only (first form,
- * gcm_batch_kernel); 16 no record loads/stores, 32 no AES, 48 both (gcm_lane_kernel). */
+ * gcm_batch_kernel); 16 no record loads/stores, 32 no AES, 48 both, 64 no GHASH, 80 AES only, 96 loads/stores only
+ * (gcm_lane_kernel). */
 void cmpi_debug_set_gcm_ablation(int mode);
 /* CTR kernel occupancy experiment: dynamic LDS bytes requested (65536..163840; more than
  * 80 KiB forces one 1024-thread block per CU). */

@@ -23,7 +23,8 @@ def timeit(fn, n=4, rounds=7):
     ts.sort(); return round(ts[len(ts)//2] * 1000, 1)
 modes = [(0, "full"), (1, "noghash"), (2, "noaes"), (3, "neither"), (8, "prologue"), (4, "full_coal"), (7, "neither_coal")]
 if os.environ.get("LANE") == "1":  # the round-2 lane kernel's ablations
-    modes = [(0, "full"), (16, "nomem"), (32, "noaes"), (48, "nomem_noaes")]
+    modes = [(0, "full"), (16, "nomem"), (32, "noaes"), (48, "nomem_noaes"), (64, "noghash"), (80, "aes_only"),
+             (96, "mem_only")]
 for m, name in modes:
     L.cmpi_debug_set_gcm_ablation(m)
     res[name] = timeit(w.seal)
