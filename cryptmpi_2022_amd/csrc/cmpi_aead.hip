@@ -251,6 +251,7 @@ std::atomic<int> g_force_L{0};
 std::atomic<uint32_t> g_force_nseg{0};
 std::atomic<int> g_gcm_mem{0};        // lane kernel record-data cache policy: bit 0 nt loads, bit 1 nt stores
 std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4/6
+std::atomic<int> g_gcm_aw{0};         // GCM lane kernel: sector-aligned windows where legal (gcm_lane_kernel AW; opt-in)
 std::atomic<int> g_gcm_form{0};       // GCM lane plan: 0 gcm_lane_kernel, 1 the first form gcm_batch_kernel
 std::atomic<int> g_wide_chw{1};       // wide plan, host-keyed: barrier-free FLOW kernel with chunk weights (1) or weights in the combine (0)
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
@@ -439,7 +440,11 @@ int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size
   // default: the round-2 lane kernel; the first form stays behind the A/B / ablation knobs
   const bool first_form = g_gcm_form.load() == 1 || g_gcm_pf.load() != 2 || g_gcm_mem.load() != 0 ||
                           (!DEC && g_gcm_ablation.load() != 0 && g_gcm_ablation.load() < 16) || (a.sched & 8192u);
-  auto fn = first_form ? cmpi::dev::gcm_batch_kernel<L, DEC> : cmpi::dev::gcm_lane_kernel<L, DEC>;
+  // sector-aligned windows (gcm_lane_kernel AW): 16-B-aligned records, one segment, nrec % 64 == 0
+  const bool aw = L == 4 && g_gcm_aw.load() && a.nseg == 1 && a.nrec % 64u == 0 &&
+                  ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.out) | a.in_stride | a.out_stride) & 15u) == 0;
+  auto fn = first_form ? cmpi::dev::gcm_batch_kernel<L, DEC>
+                       : aw ? cmpi::dev::gcm_lane_kernel<L, DEC, 1, 0, true> : cmpi::dev::gcm_lane_kernel<L, DEC>;
   if constexpr (!DEC) {  // ablations of the round-2 form (tools/ablate_split.py): 16 no memory, 32 no AES
     switch (g_gcm_ablation.load()) {
       case 16: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 1>; break;
@@ -1305,7 +1310,7 @@ int cmpi_host_unregister(void* ptr) {
   return CMPI_OK;
 }
 
-void cmpi_debug_set_sched(int mode) { g_sched.store(mode & (7 | 4096 | 8192 | 16384)); }
+void cmpi_debug_set_sched(int mode) { g_sched.store(mode & (7 | 4096 | 8192 | 16384 | 32768)); }
 void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)16 << 20)); }
 void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 127); }
 
@@ -1349,7 +1354,10 @@ void cmpi_debug_event_free(void* ev) {
 }
 void cmpi_debug_set_wide_probe(void* buf) { g_wide_probe.store(reinterpret_cast<uint64_t*>(buf)); }
 
-void cmpi_debug_set_gcm_form(int form) { g_gcm_form.store(form == 1 ? 1 : 0); }
+void cmpi_debug_set_gcm_form(int form) {
+  g_gcm_form.store(form == 1 ? 1 : 0);
+  g_gcm_aw.store(form == 3 ? 1 : 0);
+}
 void cmpi_debug_set_gcm_prefetch(int slots) { g_gcm_pf.store(slots == 3 || slots == 4 || slots == 6 ? slots : 2); }
 
 void cmpi_debug_force_wide(int mode, uint32_t steps) {

@@ -15,6 +15,8 @@
 // The arithmetic it implements is BoringSSL's aead_aes_gcm seal/open behind
 // EVP_AEAD_CTX_seal/open (aead.h:256-285) — SP 800-38D with a 96-bit IV, no AAD.
 #pragma once
+#include <type_traits>
+
 #include "aes_device.hpp"
 
 namespace cmpi {
@@ -370,7 +372,35 @@ __global__ __launch_bounds__(1024) void gcm_batch_kernel(GcmArgs a) {
 // PF = 1 (one input block in flight per lane, loaded a whole slot ahead) is the default: with PF = 2
 // the kernel needed 128 VGPRs and spilled 19 to scratch (per-record scratch traffic measured as
 // +13 MB reads / +16 MB writes per config-2 launch); at PF = 1 it has 97 VGPRs, no spills.
-template <int L, bool DECRYPT, int PF = 1, int ABL = 0>
+// AW (L = 4, one segment per record, 16-B-aligned records, nrec % 64 == 0 — the host checks):
+// sector-aligned windows on both sides.  Dense ct||tag records (n + 16 apart) start at every
+// 16-B phase, so with lane q owning slots q, q+4, .. each store instruction split every record's
+// 64 bytes over two half-written 64-B output sectors, and the L2 wrote many of them back
+// before the other half arrived (config-2 seal: 97 MB written per launch vs 68 MB algorithmic;
+// the same kernel sealing into 64-B-aligned records wrote 81 MB).  With AW, store window i of a
+// record covers slots 4i - phi .. 4i - phi + 3 (phi = the output's 16-B phase: whole sectors),
+// load window k covers 4k - psi .. (psi = the input's phase: whole sectors), and the quad
+// rotates the loaded blocks into place with DPP quad permutes (lane q <- lane (q + psi - phi) & 3
+// of load window i or i + 1).  The rotation must be wave-uniform, so records are dealt to waves
+// by residue mod 4 (the phases of equal-stride records repeat with period 4): wave w of a
+// 64-record block takes records base + 4k + w.
+template <int M>
+__device__ __forceinline__ uint32_t qrot(uint32_t x) {  // lane q <- lane (q + M) & 3 of its quad
+  constexpr int pat = (M & 3) | (((1 + M) & 3) << 2) | (((2 + M) & 3) << 4) | (((3 + M) & 3) << 6);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, pat, 0xF, 0xF, false);
+}
+template <int M>
+__device__ __forceinline__ u32x4 qsel(u32x4 x, u32x4 y, bool hi) {
+  u32x4 r;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t a = M ? qrot<M>(x[c]) : x[c], b = M ? qrot<M>(y[c]) : y[c];
+    r[c] = hi ? b : a;
+  }
+  return r;
+}
+
+template <int L, bool DECRYPT, int PF = 1, int ABL = 0, bool AW = false>
 __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
   const bool prb = a.probe && threadIdx.x == 0u;
   if (prb) a.probe[blockIdx.x * 8u + 0u] = wall_clock64();
@@ -397,8 +427,9 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
   uint32_t done = 0;  // slots this wave has started (progress_prio)
   const uint32_t groups_per_iter = (gridDim.x * blockDim.x) / (uint32_t)L;
   for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / (uint32_t)L; g < a.ngroups; g += groups_per_iter) {
-    const uint32_t r = (a.nseg == 1) ? g : g / a.nseg;
-    const uint32_t s = g - r * a.nseg;
+    // AW: records dealt to waves by residue mod 4 (one segment per record)
+    const uint32_t r = AW ? ((g & ~63u) | ((g & 15u) << 2) | ((g >> 4) & 3u)) : (a.nseg == 1) ? g : g / a.nseg;
+    const uint32_t s = AW ? 0u : g - r * a.nseg;
     const uint32_t x0 = (s == 0) ? 0u : a.r0 + (s - 1u) * a.G;
     const uint32_t x1 = a.r0 + s * a.G;
     const uint32_t nxs = x1 - x0;                      // X-blocks in this segment
@@ -436,7 +467,43 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
       acc = ((ABL & 4) ? acc : gmul_byte(acc, gl)) ^ (DECRYPT ? v : o);
     };
     uint32_t u = q;
-    if (nfull > 0u) {
+    uint32_t qs = q;  // the lane's slot residue: it owns the slots u = qs (mod L)
+    if constexpr (AW) {
+      const bool ph = !(a.sched & 32768u);  // A/B: bit 15 keeps the record mapping, drops the phases
+      const uint32_t phi = ph ? (uint32_t)(reinterpret_cast<uintptr_t>(out_rec) >> 4) & 3u : 0u;  // wave-uniform
+      const uint32_t psi = ph ? (uint32_t)(reinterpret_cast<uintptr_t>(in_rec) >> 4) & 3u : 0u;
+      qs = (q - phi) & 3u;
+      // slot 4i - phi + q sits in load window i + e, lane (q + psi - phi) & 3, e = floor((q + psi - phi) / 4)
+      const int32_t emin = psi >= phi ? 0 : -1;
+      const bool hi = (((int32_t)q + (int32_t)psi - (int32_t)phi) >> 2) != emin;  // takes window i + emin + 1
+      const uint32_t m = __builtin_amdgcn_readfirstlane((psi - phi) & 3u);
+      auto ldw = [&](int32_t k) -> u32x4 {  // load window k: slot 4k - psi + q, clamped to a full block
+        if (ABL & 1) return u32x4{(uint32_t)k, x0, lane, 0u};
+        const int32_t t = 4 * k - (int32_t)psi + (int32_t)q;
+        return ld_blk(ip + 16u * ((t >= 0 && (uint32_t)t < nfull) ? (uint32_t)t : nfull - 1u));
+      };
+      // one copy of the window loop per rotation (the rotation is a DPP immediate)
+      auto windows = [&](auto mc) {
+        constexpr int M = decltype(mc)::value;
+        const uint32_t nwin = (nfull + phi + 3u) >> 2;
+        u32x4 X = ldw(emin), Y = ldw(emin + 1);
+        for (uint32_t i = 0; i < nwin; ++i) {
+          const u32x4 v = qsel<M>(X, Y, hi);
+          X = Y;
+          Y = ldw((int32_t)i + emin + 2);
+          const int32_t us = 4 * (int32_t)i - (int32_t)phi + (int32_t)q;
+          if (us >= 0 && (uint32_t)us < nfull) full((uint32_t)us, v);
+        }
+      };
+      if (nfull > 0u) {
+        switch (m) {
+          case 0: windows(std::integral_constant<int, 0>{}); break;
+          case 1: windows(std::integral_constant<int, 1>{}); break;
+          case 2: windows(std::integral_constant<int, 2>{}); break;
+          default: windows(std::integral_constant<int, 3>{}); break;
+        }
+      }
+    } else if (nfull > 0u) {
       // PF input buffers: slot u's block is reloaded with slot u + PF*L's once u is consumed;
       // loads past the full blocks are clamped to the segment's LAST full block (value unused):
       // its line was just read, so the clamped load hits L2 (clamped to the first block it
@@ -464,7 +531,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
       }
     }
     // ---- special slots: partial last block, length block, J0 (the lane's slots >= nfull)
-    for (uint32_t ut = nfull <= q ? q : q + (uint32_t)L * ((nfull - q + (uint32_t)L - 1u) / (uint32_t)L); ut < nslots;
+    for (uint32_t ut = nfull <= qs ? qs : qs + (uint32_t)L * ((nfull - qs + (uint32_t)L - 1u) / (uint32_t)L); ut < nslots;
          ut += (uint32_t)L) {
       const uint32_t j = x0 + ut;
       const bool j0 = ut >= nxs;
@@ -488,8 +555,8 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
     u32x4 f = {0u, 0u, 0u, 0u};
     if (L == 1) {
       f = gmul_byte(acc, gl);  // L = 1: byte table holds H, w = 1
-    } else if (q < nxs) {
-      const uint32_t ulast = q + (uint32_t)L * ((nxs - 1u - q) / (uint32_t)L);
+    } else if (qs < nxs) {
+      const uint32_t ulast = qs + (uint32_t)L * ((nxs - 1u - qs) / (uint32_t)L);
       const uint32_t w = nxs - ulast;  // 1..L: H^L is the Horner byte table, H^1..H^(L-1) nibble tables
       if (w == (uint32_t)L) f = gmul_byte(acc, gl);
       else f = gmul_nib(acc, kGcmNib + (w - 1u) * 8192u);
@@ -500,7 +567,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
 
     if (a.nseg > 1) {
       if (q == 0) a.partial[g] = f;
-      if (s == 0 && (nxs % (uint32_t)L) == q) a.ekj0[r] = ekj0;  // lane that owned slot nxs
+      if (s == 0 && (nxs % (uint32_t)L) == qs) a.ekj0[r] = ekj0;  // lane that owned slot nxs
       continue;
     }
     // single-segment record: finish the tag here

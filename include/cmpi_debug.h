@@ -33,8 +33,11 @@ void cmpi_debug_set_sched(int mode);
 void cmpi_debug_set_host_chunk(size_t bytes);
 /* GCM lane-group kernel: input prefetch depth in slots (2, 3, 4 or 6; anything else = 2). */
 void cmpi_debug_set_gcm_prefetch(int slots);
-/* GCM lane plan kernel: 0 = gcm_lane_kernel (default), 1 = the first form gcm_batch_kernel (also
- * selected by a prefetch depth other than 2, the cache-policy and ablation knobs, sched bit 13). */
+/* GCM lane plan kernel: 0 = gcm_lane_kernel (default), 3 = gcm_lane_kernel with sector-aligned
+ * windows where legal (writes 97 -> 81 MB per config-2 seal, ~10 % slower: off), 1 = the first
+ * form gcm_batch_kernel (also selected by a prefetch depth other than 2, the cache-policy and
+ * ablation knobs, sched bit 13).  Sched bit 15 keeps form 3's record-to-wave mapping without
+ * its phases (A/B). */
 void cmpi_debug_set_gcm_form(int form);
 /* Diagnostics: when buf (device, >= 8 x grid u64) is non-null, every gcm_wide_kernel workgroup
    writes wall-clock (100 MHz) timestamps of its phases at buf[8*block + 0..6]: start, tables

@@ -266,7 +266,56 @@ def test_output_aligned_windows(n, plan, stride_pad):
         assert st[5] == 0 and not back[5].any() and (np.delete(st, 5) == 1).all()
         assert np.array_equal(np.delete(back, 5, axis=0), np.delete(pt, 5, axis=0))
     finally:
-        L.cmpi_debug_set_sched(7)
+        L.cmpi_debug_set_sched(7 | 16384)
+
+
+def _strided(rows: np.ndarray, off: int, stride: int, fill: int) -> np.ndarray:
+    nrec, n = rows.shape
+    buf = np.full(off + nrec * stride, fill, np.uint8)
+    view = np.lib.stride_tricks.as_strided(buf[off:], shape=(nrec, n), strides=(stride, 1), writeable=True)
+    view[:] = rows
+    return buf
+
+
+@pytest.mark.parametrize("n", [0, 15, 16, 100, 1000, 1024, 1040, 4096, 4097])
+@pytest.mark.parametrize("in_off,in_pad,out_pad", [(0, 0, 0), (16, 16, 0), (48, 16, 32), (32, 0, 16)])
+@pytest.mark.parametrize("form", [3, 0])
+def test_sector_aligned_windows(n, in_off, in_pad, out_pad, form):
+    """Lane kernel with sector-aligned windows (L = 4, one segment, nrec % 64 == 0, 16-B-aligned
+    records; form 3 = opt-in, form 0 = the default kernel without them): records at every 16-B phase
+    on both sides (strides of odd and even block counts, input base offsets), DPP quad rotation of
+    the loaded blocks, records dealt to waves by residue mod 4.  Seal and open bit-exact vs the
+    oracle, gaps between records untouched, a forged record zero-filled."""
+    L = aead.N.lib()
+    L.cmpi_debug_set_gcm_form(form)
+    try:
+        aead.force_plan(4, 1)
+        nrec = 128
+        r16 = lambda x: (x + 15) // 16 * 16  # noqa: E731
+        pt = records(0x7100 + n, nrec, n)
+        nonces = random_nonces(0x7200 + n, nrec)
+        ctx = aead.AeadCtx(KEY)
+        want = oracle.gcm_seal_batch(KEY, nonces, pt)
+        in_stride, out_stride = r16(n) + in_pad, r16(n + 16) + out_pad
+        d_in = dev(_strided(pt, in_off, in_stride, 0x55))
+        out = empty(nrec * out_stride, fill=0xAA)
+        ctx.seal_batch(out, d_in[in_off:], dev(nonces), n, nrec, in_stride=in_stride, out_stride=out_stride)
+        got = host(out)[: nrec * out_stride].reshape(nrec, out_stride)
+        assert np.array_equal(got[:, : n + 16], want) and (got[:, n + 16:] == 0xAA).all()
+        forged = want.copy()
+        forged[5, n // 2 if n else n + 3] ^= 1
+        ct_stride, pt_stride = r16(n + 16) + in_pad, r16(n) + out_pad
+        d_ct = dev(_strided(forged, in_off, ct_stride, 0x33))
+        back = empty(nrec * pt_stride, fill=0xAA)
+        st = status_buf(nrec)
+        ctx.open_batch(back, d_ct[in_off:], dev(nonces), n, nrec, status=st, in_stride=ct_stride, out_stride=pt_stride)
+        b = host(back)[: nrec * pt_stride].reshape(nrec, pt_stride)
+        st = host(st)[:nrec]
+        assert st[5] == 0 and not b[5, :n].any() and (np.delete(st, 5) == 1).all()
+        assert np.array_equal(np.delete(b[:, :n], 5, axis=0), np.delete(pt, 5, axis=0))
+        assert (b[:, n:] == 0xAA).all()
+    finally:
+        L.cmpi_debug_set_gcm_form(0)
 
 
 @pytest.mark.parametrize("nrec,segments", [(3, 0), (2, 700), (1, 2)])
