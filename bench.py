@@ -831,7 +831,7 @@ def main() -> None:
         "open_GiBps_per_gpu": round(per_rank_bytes / (open_ms * 1e-3) / GIB, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "seal launch (gcm_batch_kernel<L,false>)" if w.alg == "gcm" else f"{w.alg} seal launch",
+                     "kernel": "seal launch (gcm_lane_kernel<4,false>)" if w.alg == "gcm" else f"{w.alg} seal launch",
                      "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bpl},
         "lds_roofline": lds_roofline(w, kern_ms, local) if w.alg == "gcm" else None,
         "verified_round_trip": ok,
