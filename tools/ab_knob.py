@@ -27,7 +27,7 @@ for wl in sys.argv[3:]:
     w = Workload(wl, 0, seed=3)
     t = {(v, op): [] for v in values for op in ("seal", "open")}
     alt = os.environ.get("ABK_ALT") == "1"  # bench.py's timing: seal/open alternating per step
-    for rnd in range(7):
+    for rnd in range(int(os.environ.get("ABK_ROUNDS", "7"))):
         for v in values:
             setter(v)
             if alt:
