@@ -283,16 +283,17 @@ __device__ __forceinline__ GhashLane ghash_lane() {
   return g;
 }
 
-// X · P with the [v][p] byte table of P at LDS 0: rotate X by k bytes (X'.byte t = X.byte (t+k)),
-// then 16 conflict-free ds_read_b128 at (X'.byte t) * 256 + ((t + k) & 15) * 16.
-__device__ __forceinline__ u32x4 gmul_byte(u32x4 x, const GhashLane& g) {
+// X · P (+ Y) with the [v][p] byte table of P at LDS 0: rotate X by k bytes (X'.byte t =
+// X.byte (t+k)), then 16 conflict-free ds_read_b128 at (X'.byte t) * 256 + ((t + k) & 15) * 16.
+// The addend Y seeds the XOR chain (a Horner step's next block: no separate XOR).
+__device__ __forceinline__ u32x4 gmul_byte(u32x4 x, const GhashLane& g, u32x4 y = u32x4{0u, 0u, 0u, 0u}) {
   const uint32_t y0 = __builtin_amdgcn_alignbit(x[1], x[0], g.sh);
   const uint32_t y1 = __builtin_amdgcn_alignbit(x[2], x[1], g.sh);
   const uint32_t y2 = __builtin_amdgcn_alignbit(x[3], x[2], g.sh);
   const uint32_t y3 = __builtin_amdgcn_alignbit(x[0], x[3], g.sh);
   const uint32_t z0 = g.q1 ? y1 : y0, z1 = g.q1 ? y2 : y1, z2 = g.q1 ? y3 : y2, z3 = g.q1 ? y0 : y3;
   const uint32_t w[4] = {g.q2 ? z2 : z0, g.q2 ? z3 : z1, g.q2 ? z0 : z2, g.q2 ? z1 : z3};
-  u32x4 r = {0u, 0u, 0u, 0u};
+  u32x4 r = y;
 #pragma unroll
   for (int t = 0; t < 16; t += 2) {
     const uint32_t sa = 0x0c0c0000u | ((4u + (t & 3)) << 8) | (uint32_t)(t & 3);

@@ -48,15 +48,11 @@ __device__ __forceinline__ u32x4 ctr_load(const CtrArgs& a, uint64_t v, uint64_t
 template <bool XOR_IN>
 __device__ __forceinline__ void ctr_emit(const CtrArgs& a, uint64_t j, u32x4 ks, u32x4 v) {
   const uint64_t off = j * 16u;
-  if (!XOR_IN) {
-    *reinterpret_cast<u32x4a*>(a.out + off) = ks;
-    return;
-  }
   if (off + 16u <= a.n) {
-    *reinterpret_cast<u32x4a*>(a.out + off) = v ^ ks;
-  } else {
+    *reinterpret_cast<u32x4a*>(a.out + off) = XOR_IN ? v ^ ks : ks;
+  } else {  // the last block of a length that is not a multiple of 16: its bytes only
     const uint32_t rem = (uint32_t)(a.n - off);
-    store_partial(a.out + off, load_partial(a.in + off, rem) ^ ks, rem);
+    store_partial(a.out + off, XOR_IN ? load_partial(a.in + off, rem) ^ ks : ks, rem);
   }
 }
 

@@ -464,7 +464,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
       else if (rprio) rotate_prio(done++);
       const u32x4 o = v ^ keystream(2u + x0 + u);
       if (!(ABL & 1)) st_blk(op + 16u * u, o);
-      acc = ((ABL & 4) ? acc : gmul_byte(acc, gl)) ^ (DECRYPT ? v : o);
+      acc = (ABL & 4) ? acc ^ (DECRYPT ? v : o) : gmul_byte(acc, gl, DECRYPT ? v : o);
     };
     uint32_t u = q;
     uint32_t qs = q;  // the lane's slot residue: it owns the slots u = qs (mod L)
@@ -548,7 +548,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
         store_partial(out_rec + 16u * j, o, rem);
         x = DECRYPT ? p : o;
       }
-      acc = gmul_byte(acc, gl) ^ x;
+      acc = gmul_byte(acc, gl, x);
     }
 
     // ---- weight the lane's Horner sum by H^w, w = nxs - (lane's last X slot)

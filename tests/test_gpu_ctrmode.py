@@ -77,6 +77,25 @@ def test_702_receiver_premask_and_direct(n):
         assert got == oracle.recv702(KEY, IV32, hdr, oct_, premask=use_mask)
 
 
+@pytest.mark.parametrize("n", [1, 17, 100, 1000])
+def test_702_premask_writes_only_its_bytes(n):
+    """A <= 1 KiB mask of a length that is not a multiple of 16 (recv.c:1187-1194): the keystream
+    kernel stores the last block's bytes only — nothing past mask_len changes."""
+    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
+    s = ctrmode.Sender702(ctx, IV32)
+    pt = splitmix64_bytes(n + 11, n)
+    ct = empty(n)
+    hdr = s.send(ct, dev(pt), n)[0]
+    mask = empty(n + 64, fill=0xA5)
+    ml = ctrmode.recv702_premask(ctx, IV32, hdr, mask)
+    assert ml == n
+    m = host(mask)
+    assert (m[n:] == 0xA5).all()
+    out = empty(n)
+    ctrmode.recv702(ctx, IV32, hdr, out, ct, mask=mask, mask_len=ml)
+    assert host(out)[:n].tobytes() == pt.tobytes()
+
+
 @pytest.mark.parametrize("n,mode", [(200000, b"4"), (3000, b"0"), (40000, b"1"), (3 << 20, b"1")])
 def test_702_iv_count_carry_breaks_runs(n, mode):
     """Header counters near 2^32 and IVs ending in 0xff: IV_Count's 32-bit accumulator
