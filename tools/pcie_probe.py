@@ -49,6 +49,23 @@ def chunked(k=8):
             h_dst[i * c:(i + 1) * c].copy_(d_b[i * c:(i + 1) * c], non_blocking=True)
 
 
+s3, s4 = torch.cuda.Stream(), torch.cuda.Stream()
+
+
+def split2(h2d_on=True, d2h_on=True):  # each direction as two concurrent copies on two streams
+    c = n // 2
+    for i, (sa, sb) in enumerate(((s1, s2), (s3, s4))):
+        if h2d_on:
+            with torch.cuda.stream(sa):
+                d_a[i * c:(i + 1) * c].copy_(h_src[i * c:(i + 1) * c], non_blocking=True)
+        if d2h_on:
+            with torch.cuda.stream(sb):
+                h_dst[i * c:(i + 1) * c].copy_(d_b[i * c:(i + 1) * c], non_blocking=True)
+
+
 res = {"h2d_GBps": rate(h2d, n), "d2h_GBps": rate(d2h, n), "both_GBps_each_dir": rate(both, n),
-       "chunked8_both_GBps_each_dir": rate(chunked, n)}
+       "chunked8_both_GBps_each_dir": rate(chunked, n),
+       "h2d_2streams_GBps": rate(lambda: split2(True, False), n),
+       "d2h_2streams_GBps": rate(lambda: split2(False, True), n),
+       "both_2streams_each_GBps_each_dir": rate(split2, n)}
 print(json.dumps(res))
