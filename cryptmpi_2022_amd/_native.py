@@ -113,6 +113,7 @@ _SIGS = {
     "cmpi_debug_set_gcm_form": ([_I], None),
     "cmpi_debug_set_wide_chw": ([_I], None),
     "cmpi_debug_set_flow": ([_I, _I], None),
+    "cmpi_debug_set_flow_one_wg": ([_I], None),
     "cmpi_debug_set_host_direct": ([_S], None),
     "cmpi_debug_set_host_spin": ([_I], None),
     "cmpi_debug_set_gcm_mem": ([_I], None),

@@ -256,6 +256,7 @@ std::atomic<int> g_gcm_form{0};       // GCM lane plan: 0 gcm_lane_kernel, 1 the
 std::atomic<int> g_wide_chw{1};       // wide plan, host-keyed: barrier-free FLOW kernel with chunk weights (1) or weights in the combine (0)
 std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
 std::atomic<int> g_flow_nt{1024};     // FLOW wide kernel threads per workgroup (512 / 1024), 0 = round-1 kernel
+std::atomic<int> g_flow_one_wg{1};   // FLOW kernel: one-workgroup batches finish their tags in-kernel
 std::atomic<int> g_flow_fused{0};     // FLOW wide kernel flags: bit 0 combine fused, bits 1-3 timing ablations, bit 4 round-2-first form, bit 5 no automatic 512-thread workgroups
 std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
 std::atomic<int> g_ctr_lds{65536};
@@ -561,9 +562,13 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
       const int NT = p.nt ? (int)p.nt : g_flow_nt.load();
       const int flags = g_flow_fused.load();
       const bool r4 = !(flags & 16);
-      const bool fused = (flags & 1) && nrec <= kWideCounters;
+      // every chunk of the batch in one workgroup (single small messages): the tags are finished
+      // from the workgroup's LDS aggregation in the same launch (sched bit 0 of g_flow_one_wg: A/B)
+      const bool one_wg = r4 && g_flow_one_wg.load() && waves <= (uint64_t)(NT / 64);
+      const bool fused = one_wg || ((flags & 1) && nrec <= kWideCounters);
+      a.one_wg = one_wg ? 1u : 0u;
       if (fused) {
-        if ((rc = lease.counters(&a.wcnt))) return rc;
+        if (!one_wg && (rc = lease.counters(&a.wcnt))) return rc;
         if (DEC && !status) {  // the verdicts go somewhere: the tail of the partials buffer
           a.status = reinterpret_cast<int32_t*>(ws + (size_t)nrec * p.nseg * 16);
         }
@@ -583,7 +588,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
       void* kargs[] = {&a};
       HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(NT), kargs, lds, st));
       if (fused) {
-        if (DEC) {  // zero-fill failed records after the launch (gcm_flow_kernel: cross-XCD L2s)
+        if (DEC && !one_wg) {  // zero-fill failed records after the launch (gcm_flow_kernel: cross-XCD L2s)
           hipLaunchKernelGGL(cmpi::dev::zero_failed_kernel, dim3((uint32_t)nrec), dim3(256), 0, st, out,
                              (uint64_t)out_stride, (uint32_t)len, (const int32_t*)a.status);
           HIP_TRY(hipGetLastError());
@@ -1328,6 +1333,7 @@ void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
 void cmpi_debug_set_gcm_mem(int mode) { g_gcm_mem.store(mode & 3); }
 void cmpi_debug_set_host_spin(int on) { g_host_spin.store(on ? 1 : 0); }
 
+void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }
 void cmpi_debug_set_flow(int threads, int fused) {
   g_flow_nt.store(threads == 512 || threads == 1024 ? threads : (threads == 0 ? 0 : 1024));
   g_flow_fused.store(fused);  // bit 0 fused combine; bits 1-3 timing ablations (wrong output); bit 4 !R4

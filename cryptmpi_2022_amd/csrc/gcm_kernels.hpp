@@ -66,6 +66,9 @@ struct GcmArgs {
   // FLOW kernel, fused combine: per-record arrival counters (context memory, zero between
   // launches) and, for open, the received tags / status; null = partials for gcm_combine_kernel
   uint32_t* wcnt;
+  // FLOW kernel: the whole batch is one workgroup's units (every record's chunks together): the
+  // workgroup's LDS aggregation finishes the tags, no accumulators, no second launch
+  uint32_t one_wg;
   RoundKeys rk;
 };
 
@@ -802,6 +805,7 @@ __global__ __launch_bounds__(1024) void gcm_wide_kernel(GcmArgs a) {
 // wave's partial write-through and counts per wave (one add per chunk: contended).
 constexpr uint32_t kFlowAgg = 147456u;         // R4: aggregation slots, 16 x 16 B partials + 16 x 4 B records
 constexpr uint32_t kFlowLdsR4 = kFlowAgg + 512u;
+constexpr uint32_t kFlowFail = kFlowAgg + 448u;  // one-workgroup open: per-slot failed record + 1
 __device__ __forceinline__ uint32_t flow_tab(uint32_t f) {  // R4 nibble table f (keysetup_kernels.hpp flow_nib_exp)
   return f < 8u ? f * 8192u : 131072u + (f - 8u) * 8192u;
 }
@@ -1014,7 +1018,7 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       }
       if (prb && u == blockIdx.x * wpb) a.probe[blockIdx.x * 8u + 5u] = wall_clock64();
     }
-    if (!a.wcnt) {  // partials for gcm_xor_combine_kernel
+    if (!a.wcnt && !a.one_wg) {  // partials for gcm_xor_combine_kernel
       if (u < units && lane == 0u) a.partial[u] = pw;
       continue;
     }
@@ -1022,7 +1026,11 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       if (lane == 0u) {
         lds_st128(kFlowAgg + 16u * wv, pw);
         lds_st32(kFlowAgg + 256u + 4u * wv, r);
+        lds_st32(kFlowFail + 4u * wv, 0u);
       }
+      // one workgroup, open: this wave's plaintext stores are performed before the barrier, so
+      // a zero-fill after it lands behind them in the same L2
+      if (DECRYPT && a.one_wg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       const uint32_t l = threadIdx.x;
       const uint32_t rr = l < wpb ? lds32(kFlowAgg + 256u + 4u * l) : 0xffffffffu;
@@ -1030,6 +1038,16 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
         u32x4 x = {0u, 0u, 0u, 0u};
         uint32_t cnt = 0;
         for (uint32_t j = l; j < wpb && lds32(kFlowAgg + 256u + 4u * j) == rr; ++j, ++cnt) x ^= lds128(kFlowAgg + 16u * j);
+        if (a.one_wg) {  // every chunk of record rr is in this workgroup: x is the tag
+          if (!DECRYPT) {
+            st_blk(a.out + (uint64_t)rr * a.out_stride + a.len, x);
+          } else {
+            const u32x4 d = ld_blk(a.in + (uint64_t)rr * a.in_stride + a.len) ^ x;
+            const bool ok = (d[0] | d[1] | d[2] | d[3]) == 0u;
+            a.status[rr] = ok ? 1 : 0;
+            if (!ok) lds_st32(kFlowFail + 4u * l, rr + 1u);
+          }
+        } else {
         uint64_t* ta = reinterpret_cast<uint64_t*>(a.wcnt + 8u * rr + 4u);
         __hip_atomic_fetch_xor(ta, (uint64_t)x[0] | ((uint64_t)x[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_xor(ta + 1, (uint64_t)x[2] | ((uint64_t)x[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1049,8 +1067,19 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
             a.status[rr] = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
           }
         }
+        }
       }
       __syncthreads();  // slots reused by the next round
+      if (DECRYPT && a.one_wg) {  // zero-fill the failed records (aead.h:276-278), whole workgroup
+        for (uint32_t j = 0; j < wpb; ++j) {
+          const uint32_t f = lds32(kFlowFail + 4u * j);  // rr + 1 of a failed record, else 0
+          if (!f) continue;
+          uint8_t* o = a.out + (uint64_t)(f - 1u) * a.out_stride;
+          const uint32_t full4 = a.len & ~3u;
+          for (uint32_t i = threadIdx.x * 4u; i < full4; i += NT * 4u) *reinterpret_cast<u32a*>(o + i) = 0u;
+          for (uint32_t i = full4 + threadIdx.x; i < a.len; i += NT) o[i] = 0u;
+        }
+      }
     } else {
       if (u >= units) continue;
       // publish the partial write-through, count the arrival

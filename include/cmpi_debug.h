@@ -64,6 +64,9 @@ void cmpi_debug_event_free(void* ev);
  * the round-2 first form (byte-table Horner, radix-2 tree, gmul_wave4) instead of radix-4; bit 5
  * keeps `threads` even where the planner would pick 512-thread workgroups for few chunks. */
 void cmpi_debug_set_flow(int threads, int fused);
+/* FLOW kernel: a batch whose chunks all fit one workgroup finishes its tags in-kernel (1, default)
+ * or through the XOR-combine launch (0, A/B). */
+void cmpi_debug_set_flow_one_wg(int on);
 /* Host-memory calls (cmpi_*_host) up to `bytes` of input + output records run the direct path
  * (kernel on page-locked host memory, no DMA); larger ones the 3-stream pipeline.  0 = never. */
 void cmpi_debug_set_host_direct(size_t bytes);

@@ -30,6 +30,7 @@ def _auto_plan():
     aead.force_wide(0, 0)
     aead.set_wide_chw(True)
     aead.set_flow(1024, 0)
+    aead.set_flow_one_wg(True)
     aead.N.lib().cmpi_debug_set_host_direct(DIRECT_DEFAULT)
 
 
@@ -236,6 +237,37 @@ def test_flow_kernel_forms(threads, flags, n, nrec, steps):
     assert not back[1].any() and np.array_equal(back[0], pt[0]) and np.array_equal(back[2:], pt[2:])
     ctx.rekey(key2)
     assert np.array_equal(gpu_seal(ctx, nonces, pt), oracle.gcm_seal_batch(key2, nonces, pt))
+
+
+@pytest.mark.parametrize("one_wg", [True, False])
+@pytest.mark.parametrize("threads", [1024, 512])
+@pytest.mark.parametrize("n,nrec,steps", [(1, 1, 0), (100, 3, 1), (4096, 1, 0), (4097, 5, 2), (16384, 1, 0),
+                                          (64 * 16 * 5 - 16, 3, 1), (64 * 16 * 5 - 15, 3, 1)])
+def test_flow_one_workgroup(one_wg, threads, n, nrec, steps):
+    """FLOW batches whose chunks all fit one workgroup (single small messages): with the
+    one-workgroup finish the tags come from the workgroup's LDS XOR in the same launch and a
+    forged record is zero-filled in-kernel; bit-identical to the combine launch and the oracle.
+    Shapes on both sides of the 8 / 16 units-per-workgroup edge, seal twice, forged first and
+    last records, then a clean open."""
+    aead.force_wide(1, steps)
+    aead.set_flow(threads, 32)
+    aead.set_flow_one_wg(one_wg)
+    ctx = aead.AeadCtx(KEY)
+    pt = records(0x7100 + n, nrec, n)
+    nonces = random_nonces(0x7200 + n, nrec)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    for _ in range(2):
+        assert np.array_equal(gpu_seal(ctx, nonces, pt), want), aead.gcm_plan(ctx, n, nrec)
+    forged = want.copy()
+    forged[0, n] ^= 0x01
+    forged[nrec - 1, n + 15] ^= 0x80
+    back, st = gpu_open(ctx, nonces, forged)
+    bad = {0, nrec - 1}
+    assert list(st) == [0 if i in bad else 1 for i in range(nrec)]
+    for i in range(nrec):
+        assert (not back[i].any()) if i in bad else np.array_equal(back[i], pt[i])
+    back, st = gpu_open(ctx, nonces, want)
+    assert list(st) == [1] * nrec and np.array_equal(back, pt)
 
 
 @pytest.mark.parametrize("n", [0, 15, 16, 1000, 1024, 4096, 4097])
