@@ -563,7 +563,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
       const int flags = g_flow_fused.load();
       const bool r4 = !(flags & 16);
       // every chunk of the batch in one workgroup (single small messages): the tags are finished
-      // from the workgroup's LDS aggregation in the same launch (sched bit 0 of g_flow_one_wg: A/B)
+      // from the workgroup's LDS aggregation in the same launch (cmpi_debug_set_flow_one_wg: A/B)
       const bool one_wg = r4 && g_flow_one_wg.load() && waves <= (uint64_t)(NT / 64);
       const bool fused = one_wg || ((flags & 1) && nrec <= kWideCounters);
       a.one_wg = one_wg ? 1u : 0u;

@@ -1048,25 +1048,25 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
             if (!ok) lds_st32(kFlowFail + 4u * l, rr + 1u);
           }
         } else {
-        uint64_t* ta = reinterpret_cast<uint64_t*>(a.wcnt + 8u * rr + 4u);
-        __hip_atomic_fetch_xor(ta, (uint64_t)x[0] | ((uint64_t)x[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_xor(ta + 1, (uint64_t)x[2] | ((uint64_t)x[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t old = __hip_atomic_fetch_add(a.wcnt + 8u * rr, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + cnt == a.nch) {  // every chunk of record rr is in the accumulator
-          const uint64_t lo = __hip_atomic_load(ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint64_t hi = __hip_atomic_load(ta + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(ta, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(ta + 1, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(a.wcnt + 8u * rr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const u32x4 y = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-          if (!DECRYPT) {
-            st_blk(a.out + (uint64_t)rr * a.out_stride + a.len, y);
-          } else {  // verdict only: the zero-fill of a failed record is zero_failed_kernel's
-            const u32x4 d = ld_blk(a.in + (uint64_t)rr * a.in_stride + a.len) ^ y;
-            a.status[rr] = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+          uint64_t* ta = reinterpret_cast<uint64_t*>(a.wcnt + 8u * rr + 4u);
+          __hip_atomic_fetch_xor(ta, (uint64_t)x[0] | ((uint64_t)x[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_xor(ta + 1, (uint64_t)x[2] | ((uint64_t)x[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const uint32_t old = __hip_atomic_fetch_add(a.wcnt + 8u * rr, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (old + cnt == a.nch) {  // every chunk of record rr is in the accumulator
+            const uint64_t lo = __hip_atomic_load(ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t hi = __hip_atomic_load(ta + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ta, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ta + 1, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.wcnt + 8u * rr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u32x4 y = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+            if (!DECRYPT) {
+              st_blk(a.out + (uint64_t)rr * a.out_stride + a.len, y);
+            } else {  // verdict only: the zero-fill of a failed record is zero_failed_kernel's
+              const u32x4 d = ld_blk(a.in + (uint64_t)rr * a.in_stride + a.len) ^ y;
+              a.status[rr] = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1 : 0;
+            }
           }
-        }
         }
       }
       __syncthreads();  // slots reused by the next round
