@@ -2,7 +2,8 @@
 """Single messages (the per-message EVP / 600 regime), alternating variants of the flow kernel's
 tag finish: "combine" (XOR-combine launch), "fused" (last-arriver atomics, cmpi_debug_set_flow
 flags bit 0), "one_wg" (a batch in one workgroup finishes its tags from LDS, in-kernel zero-fill;
-cmpi_debug_set_flow_one_wg).  Device-resident seal / open (HIP events over 50 calls) and pinned
+cmpi_debug_set_flow_one_wg), "one_wg1024" (the same with 1024-thread workgroups kept, so up to
+16 chunks fit one workgroup).  Device-resident seal / open (HIP events over 50 calls) and pinned
 host seal+open (wall clock), every output checked against the oracle, plus a forged tag.
 FMA_SIZES / FMA_VARIANTS (comma lists) select the cases."""
 import ctypes
@@ -24,7 +25,7 @@ L = N.lib()
 ctx = aead.AeadCtx(KEY)
 P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 res = {}
-VARIANTS = {"combine": (0, 0), "fused": (1, 0), "one_wg": (0, 1)}
+VARIANTS = {"combine": (0, 0), "fused": (1, 0), "one_wg": (0, 1), "one_wg1024": (32, 1)}  # 32: keep 1024 threads
 names = os.environ.get("FMA_VARIANTS", "combine,one_wg").split(",")
 for n in [int(x) for x in os.environ.get("FMA_SIZES", "1024,4096,16384,65536").split(",")]:
     pt = torch.randint(0, 256, (n,), dtype=torch.uint8)
