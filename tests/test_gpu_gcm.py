@@ -123,8 +123,11 @@ def test_wire_layout_naive_alltoall():
     assert np.array_equal(host(out).reshape(nrec, n), pt)
 
 
-def test_in_place():
-    n, nrec = 4096, 16
+@pytest.mark.parametrize("n,nrec", [(4096, 16), (4096, 1), (1000, 3), (1 << 20, 2)])
+def test_in_place(n, nrec):
+    """Seal and open with out == in (BoringSSL aead.h:84: seal and open may work in place): lane plan
+    (16 x 4 KiB), one-workgroup flow launches (1 x 4 KiB, 3 x 1000 B) and the multi-workgroup flow
+    plan (2 x 1 MiB); a forged record opened in place comes back zero-filled."""
     pt = records(5, nrec, n)
     nonces = random_nonces(6, nrec)
     buf = np.zeros((nrec, n + 16), np.uint8)
@@ -135,7 +138,14 @@ def test_in_place():
     assert np.array_equal(host(d).reshape(nrec, n + 16), oracle.gcm_seal_batch(KEY, nonces, pt))
     st = status_buf(nrec)
     ctx.open_batch(d, d, dev(nonces), n, nrec, status=st, in_stride=n + 16, out_stride=n + 16)
-    assert np.array_equal(host(d).reshape(nrec, n + 16)[:, :n], pt)
+    assert np.array_equal(host(d).reshape(nrec, n + 16)[:, :n], pt) and (host(st)[:nrec] == 1).all()
+    forged = oracle.gcm_seal_batch(KEY, nonces, pt)
+    forged[nrec - 1, n // 2] ^= 0x10
+    d = dev(forged)
+    ctx.open_batch(d, d, dev(nonces), n, nrec, status=st, in_stride=n + 16, out_stride=n + 16)
+    back = host(d).reshape(nrec, n + 16)[:, :n]
+    assert list(host(st)[:nrec]) == [1] * (nrec - 1) + [0]
+    assert np.array_equal(back[: nrec - 1], pt[: nrec - 1]) and not back[nrec - 1].any()
 
 
 @pytest.mark.parametrize("plan", [(0, 0), (4, 5), (1, 1)])
