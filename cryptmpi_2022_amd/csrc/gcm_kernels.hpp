@@ -982,15 +982,22 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       const bool first = ub == blockIdx.x * wpb;
       u32x4 va = first ? va0 : prefetch(0), vb = first ? vb0 : prefetch(1);
       uint32_t it = 0;
+      // E_K(J0), folded into chunk 0's partial (only lane 0's copy is used).  Chunk 0 holds the
+      // r0 = G..2G-1 leading positions, so its first step is partial whenever 64 does not divide
+      // r0 (1 MiB: 257 positions, lane 63 alone): lane 0 is idle there and encrypts J0 in that
+      // step instead of the wave paying a whole AES pass for it afterwards.
+      const bool j0_step0 = i == 0u && base < 0;
+      u32x4 ekj = {0u, 0u, 0u, 0u};
       for (uint32_t k = 0; k < steps; k += 2u) {
         if (a.sched & 1u) rotate_prio(it++);
-        consume_ks(k, va, keystream(ctr_of(k)));
+        const u32x4 ks = keystream(k == 0u && j0_step0 && lane == 0u ? 1u : ctr_of(k));
+        if (k == 0u) ekj = ks;
+        consume_ks(k, va, ks);
         va = prefetch(k + 2u);
         if (k + 1u < steps) consume_ks(k + 1u, vb, keystream(ctr_of(k + 1u)));
         vb = prefetch(k + 3u);
       }
-      u32x4 ekj = {0u, 0u, 0u, 0u};
-      if (i == 0u) ekj = keystream(1u);  // E_K(J0) folded into chunk 0's partial
+      if (!j0_step0) ekj = i == 0u ? keystream(1u) : u32x4{0u, 0u, 0u, 0u};
       if (prb && u == blockIdx.x * wpb) a.probe[blockIdx.x * 8u + 2u] = wall_clock64();
       if constexpr (R4) {
         const u32x4 M = a.chw[4u * i + 3u];  // H^(1 + (nch-1-i)C), requested before the tree
