@@ -40,6 +40,9 @@ for name, (n, nrec) in {"a2a_8x1m": (1 << 20, 8), "1x64k": (65536, 1)}.items():
         col = col[col > 0]
         if len(col):
             r[ph] = q((col - t0).double() / 100.0)
+    end = (b[:, 6] - t0).double() / 100.0
+    r["slowest_wgs"] = [int(x) for x in torch.argsort(end, descending=True)[:8]]  # rows = workgroups in order
+    r["end_of_slowest"] = [round(float(end[i]), 2) for i in r["slowest_wgs"]]
     res[name] = r
     print(name, r, flush=True)
     w.free()
