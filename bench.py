@@ -126,12 +126,126 @@ class Workload:
             return (not torch.equal(self.ct[: 1 << 24], self.pt_sample)) and torch.equal(self.pt[: 1 << 24], self.pt_sample)
         return bool((self.status == 1).all()) and torch.equal(self.back, self.pt)
 
+    def parity_cpu(self) -> dict:
+        """Independent check of the timed workload's output, outside the timed region: the bytes
+        the GPU produced in the last timed step, compared with the system OpenSSL 3 EVP (the
+        stand-in for the reference's BoringSSL, tools/cpu_baseline.c) on the same inputs.
+        GCM/OCB: ct||tag of every record (gcm*, alltoall) or of 64 records spread over the batch
+        (ocb1m), plus the GPU's open of OpenSSL's ct||tag (statuses, plaintext) with one forged
+        record (status 0, zero-filled, aead.h:276-278).  CTR: the keystream XOR at stream offset 0,
+        across the 2^32 carry of the counter's low word and at the end of the 1 GiB stream."""
+        try:
+            return parity_cpu(self)
+        except Exception as e:  # report, never hide
+            return {"parity_cpu": False, "error": repr(e)}
+
     def free(self):
         self.ctx.close()
         for a in ("_seal_call", "_open_call", "pt", "pt_sample", "ct", "back", "nonces", "status", "ws"):
             if hasattr(self, a):
                 delattr(self, a)
         torch.cuda.empty_cache()
+
+
+class OpenSSLRef:
+    """tools/libcpu_baseline.so (system OpenSSL 3 EVP AES-128-GCM/OCB/CTR): the independent
+    implementation the bench checks the GPU's bytes against (the reference's BoringSSL cannot be
+    built here)."""
+
+    def __init__(self):
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        self.C = ctypes.CDLL(os.path.join(ROOT, "tools", "libcpu_baseline.so"))
+        self.C.cb_aead_batch.argtypes = [I, I, P, P, P, S, P, S, I, ctypes.c_long, I]
+        self.C.cb_aead_batch.restype = I
+        self.C.cb_ctr.argtypes = [P, P, P, P, S, I]
+        self.C.cb_ctr.restype = I
+        self.threads = max(1, min(16, host_cpu_info()["usable"]))
+
+    def aead(self, alg: str, dec: bool, nonces: np.ndarray, inp: np.ndarray, n: int) -> tuple[np.ndarray, int]:
+        nrec = nonces.shape[0]
+        nonces = np.ascontiguousarray(nonces, np.uint8)
+        inp = np.ascontiguousarray(inp, np.uint8)
+        out = np.zeros((nrec, n if dec else n + 16), np.uint8)
+        bad = self.C.cb_aead_batch(2 if alg == "ocb" else 1, 1 if dec else 0, KEY, nonces.ctypes.data, inp.ctypes.data,
+                                   inp.shape[1], out.ctypes.data, out.shape[1], n, nrec, self.threads)
+        return out, bad
+
+    def ctr(self, ctr0: bytes, inp: np.ndarray) -> np.ndarray:
+        inp = np.ascontiguousarray(inp, np.uint8)
+        out = np.empty_like(inp)
+        cb = (ctypes.c_uint8 * 16).from_buffer_copy(ctr0)
+        assert self.C.cb_ctr(KEY, cb, inp.ctypes.data, out.ctypes.data, inp.size, self.threads) == 0
+        return out
+
+
+def ctr_add(ctr0: bytes, k: int) -> bytes:
+    """128-bit big-endian counter block + k (SP 800-38A / EVP_aes_128_ctr)."""
+    return ((int.from_bytes(ctr0, "big") + k) % (1 << 128)).to_bytes(16, "big")
+
+
+def gpu_open_check(w, ref: "OpenSSLRef", idx: np.ndarray, pt: np.ndarray, nn: np.ndarray, ct_ref: np.ndarray) -> bool:
+    """The GPU's open of OpenSSL's ct||tag for the sampled records (one tag forged): statuses
+    1 / 0, plaintext equal / zero-filled for the forged one (BoringSSL aead.h:276-278)."""
+    k, n = len(idx), w.n
+    forged = ct_ref.copy()
+    forged[k // 2, n] ^= 0x01
+    d_in = torch.from_numpy(forged.reshape(-1)).to(w.dev)
+    d_n = torch.from_numpy(np.ascontiguousarray(nn).reshape(-1)).to(w.dev)
+    d_out = torch.full((k * n,), 0xA5, dtype=torch.uint8, device=w.dev)
+    st = torch.full((k,), 7, dtype=torch.int32, device=w.dev)
+    ctx = w.ctx
+    ws = ctx.workspace_size(n, k)
+    d_ws = torch.empty(max(ws, 16), dtype=torch.uint8, device=w.dev) if ws else None
+    fn = ctx.open_batch
+    try:
+        fn(d_out, d_in, d_n, n, k, status=st, workspace=d_ws)
+    except Exception:
+        pass  # a failed record raises after the launch (CMPI_EAUTH); the statuses tell which
+    torch.cuda.synchronize(w.dev)
+    got = d_out.view(k, n).cpu().numpy()
+    sts = st.cpu().numpy()
+    want_st = np.ones(k, np.int32)
+    want_st[k // 2] = 0
+    want = pt.copy()
+    want[k // 2] = 0
+    return bool(np.array_equal(sts, want_st) and np.array_equal(got, want))
+
+
+def parity_cpu(w) -> dict:
+    """See Workload.parity_cpu."""
+    ref = OpenSSLRef()
+    torch.cuda.synchronize(w.dev)
+    n, N = w.n, w.nrec
+    if w.alg == "ctr":
+        windows = {}
+        span = 1 << 24  # 16 MiB windows
+        lo = int.from_bytes(w.ctr0[12:], "big")
+        carry_blk = (1 << 32) - lo  # first block whose low counter word wrapped
+        offs = {"offset_0": 0, "across_2^32_carry": max(0, min(carry_blk * 16 - span // 2, n - span)), "end": n - span}
+        ok = True
+        for name, off in offs.items():
+            off -= off % 16
+            pt = w.pt[off: off + span].cpu().numpy()
+            got = w.ct[off: off + span].cpu().numpy()
+            want = ref.ctr(ctr_add(w.ctr0, off // 16), pt)
+            eq = bool(np.array_equal(got, want))
+            windows[name] = {"byte_offset": off, "bytes": span, "equal": eq}
+            ok = ok and eq
+        return {"parity_cpu": ok, "ref": "OpenSSL 3 EVP_aes_128_ctr", "ctr0": w.ctr0.hex(),
+                "carry_block": carry_blk, "windows": windows}
+    k = N if n * N <= (256 << 20) else 64  # every record, or 64 spread over the batch
+    idx = np.linspace(0, N - 1, k).round().astype(np.int64) if k < N else np.arange(N)
+    it = torch.from_numpy(idx).to(w.dev)
+    pt = w.pt.view(N, n).index_select(0, it).cpu().numpy()
+    nn = w.nonces.view(N, 12).index_select(0, it).cpu().numpy()
+    got = w.ct.view(N, n + 16).index_select(0, it).cpu().numpy()
+    want, bad = ref.aead(w.alg, False, nn, pt, n)
+    seal_ok = bad == 0 and bool(np.array_equal(got, want))
+    nbad = int((got != want).any(axis=1).sum())
+    open_ok = gpu_open_check(w, ref, idx[: min(k, 256)], pt[:256], nn[:256], want[:256])
+    return {"parity_cpu": seal_ok and open_ok, "ref": f"OpenSSL 3 EVP_aes_128_{w.alg}",
+            "records_checked": int(k), "of": int(N), "seal_ct_tag_equal": seal_ok, "records_differing": nbad,
+            "gpu_open_of_ref_ct_with_one_forged": open_ok}
 
 
 # Secondary workloads (extras): enough warm-up for the clock to leave its idle state (10 steps
@@ -357,19 +471,28 @@ def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, wa
     torch.cuda.synchronize(dev)
     barrier()
     wall = time.perf_counter() - t0
+    # parity (outside the timed region): this rank's wire blocks of the last call, nonce||ct||tag,
+    # against OpenSSL's seal of the same blocks under the nonces the wire carries
+    try:
+        wv = wire.view(nblk, n + 28).cpu().numpy()
+        want, bad = OpenSSLRef().aead("gcm", False, wv[:, :12], send.view(nblk, n).cpu().numpy(), n)
+        par = bad == 0 and bool(np.array_equal(wv[:, 12:], want))
+    except Exception:
+        par = False
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if pg is not None and p > 1:
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        okt = torch.tensor([1 if ok else 0, 1 if par else 0], dtype=torch.int32, device=dev)
         pg.all_reduce(okt, op=pg.ReduceOp.MIN)
-        ok = bool(okt.item())
+        ok, par = bool(okt[0].item()), bool(okt[1].item())
     wall = float(t.item())
     ctx.close()
     return {"ranks": p, "blocks_per_rank": nblk, "block_bytes": n, "ms_per_call": round(wall / steps * 1e3, 4),
             "GiBps_per_rank": round(nblk * n * steps / wall / GIB, 2),
             "GiBps_all_ranks": round(p * nblk * n * steps / wall / GIB, 2),
             "transport": "RCCL all_to_all_single (xGMI)" if p > 1 else "1 rank: device copy (blocks looped back)",
-            "all_blocks_authenticated": ok}
+            "all_blocks_authenticated": ok, "parity_cpu": par,
+            "parity": "every rank's wire blocks (nonce||ct||tag) vs OpenSSL 3 EVP_aes_128_gcm seal under the wire nonces"}
 
 
 def config1_message(device: int, n: int = 64 << 10, iters: int = 200) -> dict:
@@ -806,6 +929,7 @@ def main() -> None:
     w = Workload(args.workload, local, seed=1000 + rank)
     wall, seal_ms, open_ms = time_steps(w, args.steps, args.warmup, barrier)
     ok = w.verify()
+    parity = w.parity_cpu() if rank == 0 else None  # outside the timed region
     per_rank_bytes = w.n * w.nrec  # plaintext bytes per step per rank
     wall_max, value = aggregate(wall, per_rank_bytes, args.steps, pg, w.dev)
     bpl = w.bytes_per_launch()
@@ -835,6 +959,8 @@ def main() -> None:
                      "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bpl},
         "lds_roofline": lds_roofline(w, kern_ms, local) if w.alg == "gcm" else None,
         "verified_round_trip": ok,
+        "parity_cpu": None if parity is None else parity["parity_cpu"],
+        "parity": parity,
     }
     w.free()
     if rank == 0:
@@ -866,6 +992,9 @@ def main() -> None:
                                 "open_GiBps": round(we.n * we.nrec / (o_ms * 1e-3) / GIB, 2),
                                 "seal_hbm_frac": round(we.bytes_per_launch() / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                 "verified": we.verify()}
+                par = we.parity_cpu()
+                extras[name]["parity_cpu"] = par["parity_cpu"]
+                extras[name]["parity"] = par
                 we.free()
             except Exception as e:  # report, never hide
                 extras[name] = {"error": repr(e)}

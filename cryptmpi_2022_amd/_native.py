@@ -92,14 +92,14 @@ _SIGS = {
     "cmpi_600_seal": ([_P, _P, _P, _P, _S, _P], _I),
     "cmpi_600_open": ([_P, _P, _P, _S, _P, _P], _I),
     "cmpi_700_send": ([_P, _P, _P, _P, _S, _P, _P, _P], _I),
-    "cmpi_700_recv": ([_P, _P, _P, _P, _P, _P], _I),
+    "cmpi_700_recv": ([_P, _P, _P, _P, _S, _P, _P], _I),
     "cmpi_702_sender_new": ([_P, _P, _S, _I, _P], _P),
     "cmpi_702_sender_free": ([_P], None),
     "cmpi_702_sender_state": ([_P, _P], _I),
     "cmpi_702_send": ([_P, _I, _P, _S, _P, _P, _P], _I),
     "cmpi_702_precompute": ([_P, _S, _I, _P], _I),
     "cmpi_702_recv_premask": ([_P, _P, _P, _P, _S, _P, _P], _I),
-    "cmpi_702_recv": ([_P, _P, _P, _P, _P, _P, _S, _P], _I),
+    "cmpi_702_recv": ([_P, _P, _P, _P, _S, _P, _P, _S, _P], _I),
     "cmpi_gcm_seal_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P], _I),
     "cmpi_gcm_open_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
     "cmpi_ocb_seal_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P], _I),

@@ -379,21 +379,20 @@ int get_mj(const cmpi_ctx* c, uint32_t G, cmpi::dev::GcmCombineArgs& ca) {
 // j < 4 (the weights of chunk i's four quarter-wave sums, so the combine only XORs): built on
 // the host from H once per (C, nch) and kept in HBM for the context's lifetime.  Device-keyed
 // contexts (no host H) return null and keep the barrier-phased kernel + combine weighting.
-// At most kChwCache entries per context (record lengths vary in the per-message regimes): a
-// full cache is dropped as a whole (hipFree orders itself after the work in flight).  The copy is
-// stream-ordered on the launch stream; the host vector is pageable, so hipMemcpyAsync has staged
-// it before returning.
+// At most kChwCache entries per context (record lengths vary in the per-message regimes).  A
+// cached entry is uploaded with a blocking copy before it is published, so a call on another
+// stream that finds it can never launch before its bytes are in HBM, and cached entries are freed
+// only with the context (or at a re-key, which the caller orders after all use).  Past the cap,
+// the weights of one call go to a stream-ordered allocation on the launch stream that the caller
+// releases with hipFreeAsync after its launches (*transient = true) — ADVICE r2.
 constexpr size_t kChwCache = 32;
-int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out, hipStream_t st) {
+int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out, hipStream_t st, bool* transient) {
   *out = nullptr;
+  *transient = false;
   if (c->dev_keys) return CMPI_OK;
   std::lock_guard<std::mutex> lk(c->mu);
   auto key = std::make_pair(C, nch);
   auto it = c->chw.find(key);
-  if (it == c->chw.end() && c->chw.size() >= kChwCache) {
-    for (auto& kv : c->chw) (void)hipFree(kv.second);
-    c->chw.clear();
-  }
   if (it == c->chw.end()) {
     std::vector<Blk> w((size_t)nch * 4);
     const Blk P = cmpi::gf_pow(c->H, C), H16 = cmpi::gf_pow(c->H, 16);
@@ -407,8 +406,18 @@ int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out, hipS
       wi = cmpi::gf_mul(wi, P);
     }
     void* d = nullptr;
+    if (c->chw.size() >= kChwCache) {  // transient: stream-ordered, freed by the caller after its launches
+      if (hipMallocAsync(&d, (size_t)nch * 64, st) != hipSuccess) return fail(CMPI_ENOMEM, "hipMallocAsync chunk weights failed");
+      if (hipMemcpyAsync(d, w.data(), (size_t)nch * 64, hipMemcpyHostToDevice, st) != hipSuccess) {
+        (void)hipFreeAsync(d, st);
+        return fail(CMPI_EHIP, "chunk weights copy failed");
+      }
+      *out = reinterpret_cast<const u32x4*>(d);
+      *transient = true;
+      return CMPI_OK;
+    }
     if (hipMalloc(&d, (size_t)nch * 64) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc chunk weights failed");
-    if (hipMemcpyAsync(d, w.data(), (size_t)nch * 64, hipMemcpyHostToDevice, st) != hipSuccess) {
+    if (hipMemcpy(d, w.data(), (size_t)nch * 64, hipMemcpyHostToDevice) != hipSuccess) {  // complete before publishing
       (void)hipFree(d);
       return fail(CMPI_EHIP, "chunk weights copy failed");
     }
@@ -552,8 +561,17 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.nch = p.nseg;
     int rc = get_h64tab(c, &a.htab);
     if (!rc) rc = get_wnib(c, &a.wtab);
-    if (!rc && g_wide_chw.load() && !(a.sched & 8u)) rc = get_chw(c, p.G, p.nseg, &a.chw, st);
+    bool chw_transient = false;
+    if (!rc && g_wide_chw.load() && !(a.sched & 8u)) rc = get_chw(c, p.G, p.nseg, &a.chw, st, &chw_transient);
     if (rc) return rc;
+    // a transient weights buffer is released in stream order after this call's launches
+    struct FreeAsync {
+      const void* p;
+      hipStream_t s;
+      ~FreeAsync() {
+        if (p) (void)hipFreeAsync(const_cast<void*>(p), s);
+      }
+    } chw_guard{chw_transient ? (const void*)a.chw : nullptr, st};
     a.probe = g_wide_probe.load();
     const uint64_t waves = (uint64_t)nrec * p.nseg;
     if (a.chw && g_flow_nt.load()) {

@@ -130,10 +130,12 @@ int cmpi_700_send(const cmpi_ctx* c, const uint8_t send_iv[16], uint64_t* counte
 }
 
 int cmpi_700_recv(const cmpi_ctx* c, const uint8_t recv_iv[16], const uint8_t header[26], uint8_t* out,
-                  const uint8_t* in, void* stream) {
+                  size_t out_cap, const uint8_t* in, void* stream) {
   if (!c || !recv_iv || !header) return fail(CMPI_EINVAL, "null argument");
   const uint32_t totaldata = be32h(header);
   if (totaldata && (!in || !out)) return fail(CMPI_EINVAL, "null buffer");
+  // the length comes from the wire: bounded by the caller's buffer (the reference trusts it)
+  if (totaldata > out_cap) return fail(CMPI_EINVAL, "header announces %u bytes, out holds %zu", totaldata, out_cap);
   uint8_t iv[16];
   memcpy(iv, recv_iv, 16);
   cmpi_iv_count(iv, be32h(header + 5));  // recv.c:867-871
@@ -226,9 +228,8 @@ int cmpi_702_send(cmpi_702_sender* s, int pending, const uint8_t* in, size_t n, 
   DeviceGuard dg(s->ctx->device);
   int rc;
   if (totaldata < kPreCom) {  // :1689-1731
-    if (r->compute_size >= totaldata) {  // encryption_common_counter (ring_host.hpp), stream A
-      lk.unlock();                        // it takes the ring lock itself
-      rc = cmpi_ctr_ring_encrypt(r, out, in, n, stream);
+    if (r->compute_size >= totaldata) {  // encryption_common_counter (ring_host.hpp), stream A,
+      rc = ring_encrypt_locked(r, out, in, n, stream);  // under the lock that chose it
       return rc ? rc : 1;
     }
     uint8_t iv[16];
@@ -286,6 +287,8 @@ int cmpi_702_precompute(cmpi_702_sender* s, size_t n, int rounds, void* stream) 
   cmpi_ctr_ring* r = s->ring;
   std::lock_guard<std::mutex> lk(r->mu);
   DeviceGuard dg(s->ctx->device);
+  RingOrder ord{r, (hipStream_t)stream};  // ring fills chain after the ring's previous use
+  if (int e = ord.begin()) return e;
   for (int i = 0; i < rounds; ++i) {  // :1919-1979
     if (!((r->compute_size + th_data * segments_no) <= (r->max - 16) && (pre_com_data + th_data * segments_no <= totaldata)))
       break;
@@ -342,11 +345,12 @@ int cmpi_702_recv_premask(const cmpi_ctx* c, const uint8_t recv_iv[32], const ui
 }
 
 int cmpi_702_recv(const cmpi_ctx* c, const uint8_t recv_iv[32], const uint8_t header[26], uint8_t* out,
-                  const uint8_t* in, const uint8_t* mask, size_t mask_len, void* stream) {
+                  size_t out_cap, const uint8_t* in, const uint8_t* mask, size_t mask_len, void* stream) {
   if (!c || !recv_iv || !header) return fail(CMPI_EINVAL, "null argument");
   const int totaldata = (int)be32h(header);
   if (totaldata < 0) return fail(CMPI_EINVAL, "malformed header");
   if (totaldata == 0) return CMPI_OK;
+  if ((size_t)totaldata > out_cap) return fail(CMPI_EINVAL, "header announces %d bytes, out holds %zu", totaldata, out_cap);
   if (!out || !in) return fail(CMPI_EINVAL, "null buffer");
   const unsigned long c0 = be32h(header + 5);
   DeviceGuard dg(c->device);
@@ -360,7 +364,10 @@ int cmpi_702_recv(const cmpi_ctx* c, const uint8_t recv_iv[32], const uint8_t he
     return ctr_launch(c, out, in, (size_t)totaldata, iv, stream);
   }
   const int chop = (int)be32h(header + 21);
-  if (chop <= 0) return fail(CMPI_EINVAL, "malformed header (choping_sz)");
+  // a sender's choping_sz is a multiple of 16 in [16, totaldata rounded up to 16] (send.c:1595-1637);
+  // anything else would size the slice list from untrusted bytes
+  if (chop < 16 || chop % 16 || (int64_t)chop > ((int64_t)totaldata + 15) / 16 * 16)
+    return fail(CMPI_EINVAL, "malformed header (choping_sz %d for %d bytes)", chop, totaldata);
   int segments_no = (totaldata > kPipe && totaldata > kLarge) ? 1 + (totaldata - kPipe - 1) / kPipe + 1 : 1;
   if (header[20] == '3' || header[20] == '4') segments_no = 1;  // recv.c:1237-1238
   std::vector<CtrSlice> v;  // recv.c:1328-1399

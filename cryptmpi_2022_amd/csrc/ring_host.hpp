@@ -12,6 +12,11 @@ struct cmpi_ctr_ring {
   int max = 0, start = 0, end = 0, compute_size = 0;
   unsigned long counter = 0, counter_needto_send = 0;
   std::mutex mu;
+  // every ring operation is ordered after the previous one (a fill on one stream, the XOR that
+  // consumes it on another) by this event; the ring's free waits for it alone, not the device
+  hipEvent_t last = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool used = false;
 };
 
 namespace {
@@ -32,6 +37,23 @@ int ring_ctr(const cmpi_ctr_ring* r, unsigned long counter, uint8_t* out, const 
   cmpi_iv_count(cb, counter);
   return ctr_launch(r->ctx, out, in, n, cb, stream);
 }
+
+// Ring operations chain on r->last (called with r->mu held): the launch stream waits for the
+// previous operation when it ran on another stream, and records the new last use after.
+struct RingOrder {
+  cmpi_ctr_ring* r;
+  hipStream_t st;
+  int begin() {
+    if (r->used && r->last_stream != st) HIP_TRY(hipStreamWaitEvent(st, r->last, 0));
+    return CMPI_OK;
+  }
+  ~RingOrder() {
+    if (hipEventRecord(r->last, st) == hipSuccess) {
+      r->used = true;
+      r->last_stream = st;
+    }
+  }
+};
 
 }  // namespace
 
@@ -60,13 +82,20 @@ cmpi_ctr_ring* cmpi_ctr_ring_new(const cmpi_ctx* ctx, const uint8_t iv[16], size
     delete r;
     return nullptr;
   }
+  if (hipEventCreateWithFlags(&r->last, hipEventDisableTiming) != hipSuccess) {
+    fail(CMPI_EHIP, "hipEventCreate failed");
+    (void)hipFree(r->dring);
+    delete r;
+    return nullptr;
+  }
   return r;
 }
 
 void cmpi_ctr_ring_free(cmpi_ctr_ring* r) {
   if (!r) return;
   DeviceGuard dg(r->ctx->device);
-  (void)hipDeviceSynchronize();  // ring fills / consumptions may still be in flight
+  if (r->used) (void)hipEventSynchronize(r->last);  // the ring's last fill / consumption
+  if (r->last) (void)hipEventDestroy(r->last);
   if (r->dring) (void)hipFree(r->dring);
   delete r;
 }
@@ -91,6 +120,8 @@ int cmpi_ctr_ring_generate(cmpi_ctr_ring* r, size_t gen_bytes, void* stream) {
   DeviceGuard dg(r->ctx->device);
   const int gen = (int)gen_bytes;
   if (!(r->compute_size <= (r->max - gen - 1024))) return 0;
+  RingOrder ord{r, (hipStream_t)stream};
+  if (int e = ord.begin()) return e;
   int blockamount = ((gen - 1) / 16) * 16 + 16;
   int rc;
   auto fill = [&](int amount) {
@@ -119,16 +150,20 @@ int cmpi_ctr_ring_generate(cmpi_ctr_ring* r, size_t gen_bytes, void* stream) {
   return rc ? rc : 1;
 }
 
-// send.c:1273-1465
-int cmpi_ctr_ring_encrypt(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_t n, void* stream) {
-  if (!r) return fail(CMPI_EINVAL, "null ring");
+}  // extern "C"
+
+namespace {
+// send.c:1273-1465, with r->mu held by the caller (cmpi_ctr_ring_encrypt, and cmpi_702_send, whose
+// stream choice and header counter must see the same ring state as the XOR that follows)
+int ring_encrypt_locked(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_t n, void* stream) {
   // n == 0 is not a no-op: like the reference, it retires one 16-byte ring block
   // (((0 - 1) / 16) * 16 + 16 == 16, send.c:1331-1335).
   if (n && (!out || !in)) return fail(CMPI_EINVAL, "null buffer");
   if (n > 0x7FFFFFFFu) return fail(CMPI_EINVAL, "message larger than INT_MAX");
-  std::lock_guard<std::mutex> lk(r->mu);
   DeviceGuard dg(r->ctx->device);
   hipStream_t st = (hipStream_t)stream;
+  RingOrder ord{r, st};
+  if (int e = ord.begin()) return e;
   const int enc_datasize = (int)n;
   int how_much_generate, temporary_datasize, datasize;
   if (enc_datasize > r->compute_size) {
@@ -173,6 +208,15 @@ int cmpi_ctr_ring_encrypt(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, siz
     r->counter_needto_send += (unsigned long)(((how_much_generate - 1) / 16) + 1);
   }
   return CMPI_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int cmpi_ctr_ring_encrypt(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_t n, void* stream) {
+  if (!r) return fail(CMPI_EINVAL, "null ring");
+  std::lock_guard<std::mutex> lk(r->mu);
+  return ring_encrypt_locked(r, out, in, n, stream);
 }
 
 // recv.c:954-1023

@@ -26,8 +26,8 @@ def send700(ctx, send_iv: bytes, counter: int, out, inp, n: int, stream=None):
 
 
 def recv700(ctx, recv_iv: bytes, header: bytes, out, inp, stream=None) -> None:
-    N.check(N.lib().cmpi_700_recv(ctx.handle, _b(recv_iv, 16), _b(header, HEADER), _dptr(out), _dptr(inp),
-                                  _stream_ptr(stream)))
+    N.check(N.lib().cmpi_700_recv(ctx.handle, _b(recv_iv, 16), _b(header, HEADER), _dptr(out),
+                                  out.numel() if out is not None else 0, _dptr(inp), _stream_ptr(stream)))
 
 
 class Sender702:
@@ -79,5 +79,6 @@ def recv702_premask(ctx, recv_iv: bytes, header: bytes, mask, stream=None) -> in
 
 
 def recv702(ctx, recv_iv: bytes, header: bytes, out, inp, mask=None, mask_len: int = 0, stream=None) -> None:
-    N.check(N.lib().cmpi_702_recv(ctx.handle, _b(recv_iv, 32), _b(header, HEADER), _dptr(out), _dptr(inp),
-                                  _dptr(mask), mask_len, _stream_ptr(stream)))
+    N.check(N.lib().cmpi_702_recv(ctx.handle, _b(recv_iv, 32), _b(header, HEADER), _dptr(out),
+                                  out.numel() if out is not None else 0, _dptr(inp), _dptr(mask), mask_len,
+                                  _stream_ptr(stream)))

@@ -16,8 +16,9 @@
  * Header (COUNTER_HEADER_SIZE = 26, mpiimpl.h:385): [0..3] BE32 n, [4] stream '0'/'1' (702,
  * n < 64 KiB), [5..8] BE32 counter, [20] '1'/'4' (702), [21..24] BE32 choping_sz.  Bytes the
  * reference never writes (it sends whatever its static buffer held) are zero here.
- * Data pointers are device memory, headers and IVs host memory.  Calls on one sender are
- * serialised by the caller and stream-ordered.
+ * Data pointers are device memory, headers and IVs host memory.  Calls on one sender (send,
+ * precompute) may come from several threads: the ring lock is held from the stream choice of a
+ * send to the XOR that consumes the ring; they are stream-ordered among themselves.
  */
 #ifndef CMPI_CTRMODE_H
 #define CMPI_CTRMODE_H
@@ -38,9 +39,10 @@ extern "C" {
  * (unsigned long)(n - 1) / 16 + 1 exactly as the reference's expression. */
 int cmpi_700_send(const cmpi_ctx *ctx, const uint8_t send_iv[16], uint64_t *counter, const uint8_t *in, size_t n,
                   uint8_t header[26], uint8_t *out, void *stream);
-/* recv.c:812-940: recv_iv = Recv_common_IV[source*16 .. +16). */
+/* recv.c:812-940: recv_iv = Recv_common_IV[source*16 .. +16).  out holds out_cap bytes: a header
+ * announcing more is refused (CMPI_EINVAL) — the reference trusts the wire. */
 int cmpi_700_recv(const cmpi_ctx *ctx, const uint8_t recv_iv[16], const uint8_t header[26], uint8_t *out,
-                  const uint8_t *in, void *stream);
+                  size_t out_cap, const uint8_t *in, void *stream);
 
 /* ---- 702 (pre-computed counter) ---- */
 typedef struct cmpi_702_sender cmpi_702_sender;
@@ -64,10 +66,12 @@ int cmpi_702_precompute(cmpi_702_sender *s, size_t n, int rounds, void *stream);
  * generated before the payload lands; *mask_len = bytes made (0 for n >= 64 KiB: no mask). */
 int cmpi_702_recv_premask(const cmpi_ctx *ctx, const uint8_t recv_iv[32], const uint8_t header[26], uint8_t *mask,
                           size_t mask_cap, size_t *mask_len, void *stream);
-/* recv.c:1198-1403: plaintext (device, n bytes) from the payload; mask/mask_len from
- * cmpi_702_recv_premask, or NULL/0 when the payload arrived first (direct CTR). */
+/* recv.c:1198-1403: plaintext (device, n bytes, out_cap >= n) from the payload; mask/mask_len from
+ * cmpi_702_recv_premask, or NULL/0 when the payload arrived first (direct CTR).  A header whose n
+ * exceeds out_cap, or whose choping_sz is not a multiple of 16 in [16, n rounded up to 16], is
+ * refused (CMPI_EINVAL). */
 int cmpi_702_recv(const cmpi_ctx *ctx, const uint8_t recv_iv[32], const uint8_t header[26], uint8_t *out,
-                  const uint8_t *in, const uint8_t *mask, size_t mask_len, void *stream);
+                  size_t out_cap, const uint8_t *in, const uint8_t *mask, size_t mask_len, void *stream);
 
 #ifdef __cplusplus
 }

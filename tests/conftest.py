@@ -12,6 +12,27 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
 
 
+# The BASELINE-config oracle tests run first, so that a -x stop anywhere else cannot hide them:
+# config 2 (every record), config 3 (OCB sample), config 4 (the full 1 GiB stream), config 5
+# (the naive-alltoall shape), then the 702/700 composites, the async host API and the 2-process
+# 600 exchange.  Everything else keeps its collection order.
+_FIRST = ("test_gpu_baseline_configs.py::", "test_config2_full_batch_properties", "test_ocb_config3_sample",
+          "test_ctr_config4_full_stream", "test_config5_shape_default_plan", "test_gpu_ctrmode.py::",
+          "test_gpu_async.py::", "test_gpu_p2p.py::")
+
+
+def _rank(item) -> int:
+    nid = item.nodeid
+    for i, key in enumerate(_FIRST):
+        if key in nid:
+            return i
+    return len(_FIRST)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=_rank)  # stable: ties keep the collection order
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

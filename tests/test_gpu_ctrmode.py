@@ -134,3 +134,31 @@ def test_700_sequence_vs_oracle():
         ctrmode.recv700(ctx, iv, hdr, back, out)
         assert host(back)[:n].tobytes() == pt.tobytes()
     torch.cuda.synchronize()
+
+
+def test_recv_refuses_untrusted_header_sizes():
+    """The header is wire input: a length beyond the caller's buffer, or a choping_sz
+    that is not a multiple of 16 in [16, n rounded up to 16], is refused before any launch or
+    slice list is built (the reference trusts both, recv.c:1226-1240)."""
+    from cryptmpi_2022_amd import _native as N
+
+    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
+    n = 200000
+    ct = empty(n)
+    out = empty(n - 1)  # one byte short
+    hdr = bytearray(26)
+    hdr[0:4] = n.to_bytes(4, "big")
+    hdr[20:21] = b"4"
+    hdr[21:25] = (16704).to_bytes(4, "big")
+    with pytest.raises(N.CmpiError):
+        ctrmode.recv702(ctx, IV32, bytes(hdr), out, ct)
+    with pytest.raises(N.CmpiError):
+        ctrmode.recv700(ctx, IV32[:16], bytes(hdr), out, ct)
+    out = empty(n)
+    for chop in (1, 15, 17, ((n + 15) // 16 + 1) * 16):
+        hdr[21:25] = chop.to_bytes(4, "big")
+        with pytest.raises(N.CmpiError):
+            ctrmode.recv702(ctx, IV32, bytes(hdr), out, ct)
+    hdr[21:25] = (16704).to_bytes(4, "big")
+    ctrmode.recv702(ctx, IV32, bytes(hdr), out, ct)  # a well-formed header still opens
+    assert host(out)[:n].tobytes() == oracle.recv702(KEY, IV32, bytes(hdr), host(ct)[:n].tobytes(), premask=False)
