@@ -17,7 +17,9 @@ except Exception:  # pragma: no cover - torch is always present in this image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcmpi_aead.so")
+# CMPI_LIB: the diagnostics build (tools/libcmpi_aead_tools.so, -DCMPI_TOOLS=1: kernel phase
+# probes) for tools/ scripts; everything else loads the product library.
+LIB_PATH = os.environ.get("CMPI_LIB") or os.path.join(_HERE, "libcmpi_aead.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
 CMPI_OK = 0
@@ -109,24 +111,20 @@ _SIGS = {
     "cmpi_waitall": ([_P, _S], _I),
     "cmpi_debug_force_plan": ([_I, _U32], None),
     "cmpi_debug_force_wide": ([_I, _U32], None),
-    "cmpi_debug_set_gcm_prefetch": ([_I], None),
-    "cmpi_debug_set_gcm_form": ([_I], None),
-    "cmpi_debug_set_wide_chw": ([_I], None),
-    "cmpi_debug_set_flow": ([_I, _I], None),
+    "cmpi_debug_set_flow_threads": ([_I], None),
     "cmpi_debug_set_flow_one_wg": ([_I], None),
     "cmpi_debug_set_host_direct": ([_S], None),
     "cmpi_debug_set_host_spin": ([_I], None),
-    "cmpi_debug_set_gcm_mem": ([_I], None),
     "cmpi_debug_event_new": ([], _P),
     "cmpi_debug_event_record": ([_P, _P], _I),
     "cmpi_debug_event_ms": ([_P, _P], ctypes.c_float),
     "cmpi_debug_event_free": ([_P], None),
-    "cmpi_debug_set_wide_probe": ([_P], None),
-    "cmpi_debug_set_ctr_lds": ([_I], None),
-    "cmpi_debug_set_gcm_ablation": ([_I], None),
-    "cmpi_debug_set_sched": ([_I], None),
     "cmpi_debug_set_host_chunk": ([_S], None),
     "cmpi_debug_gcm_plan": ([_P, _S, _S, _P], _I),
+}
+# only in the diagnostics build (CMPI_LIB=tools/libcmpi_aead_tools.so)
+_TOOLS_SIGS = {
+    "cmpi_debug_set_wide_probe": ([_P], None),
 }
 
 _lib = None
@@ -144,6 +142,11 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
+        for name, (args, res) in _TOOLS_SIGS.items():
+            fn = getattr(L, name, None)
+            if fn is not None:
+                fn.argtypes = args
+                fn.restype = res
         _lib = L
     return _lib
 

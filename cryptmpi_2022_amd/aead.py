@@ -264,16 +264,10 @@ def force_wide(mode: int = 0, steps: int = 0) -> None:
     N.lib().cmpi_debug_force_wide(mode, steps)
 
 
-def set_wide_chw(on: bool = True) -> None:
-    """Test hook: wide GCM plan applies the chunk weights in the wide kernel (True, default) or in
-    the combine kernel (False)."""
-    N.lib().cmpi_debug_set_wide_chw(1 if on else 0)
-
-
-def set_flow(threads: int = 1024, flags: int = 0) -> None:
-    """Test hook (cmpi_debug.h cmpi_debug_set_flow): FLOW wide-kernel workgroup size and form
-    flags (bit 0 fused combine, bit 4 round-2 first form, bit 5 no automatic 512 threads)."""
-    N.lib().cmpi_debug_set_flow(threads, flags)
+def set_flow_threads(threads: int = 0) -> None:
+    """Test hook (cmpi_debug_set_flow_threads): FLOW kernel workgroup size, 0 = automatic (512 for
+    batches of at most 8 waves per CU, else 1024), 512 or 1024 forced."""
+    N.lib().cmpi_debug_set_flow_threads(threads)
 
 
 def set_flow_one_wg(on: bool = True) -> None:

@@ -70,7 +70,6 @@ struct DeviceGuard {
 };
 
 constexpr uint32_t kGcmThreads = 1024;
-constexpr uint32_t kNibTables = 4;  // H^1..H^4
 constexpr size_t kByteTab = 4096 * 16;
 constexpr size_t kNibTab = 512 * 16;
 
@@ -80,16 +79,15 @@ struct DevTables {
   uint32_t td0[256];
   uint32_t isb[256];
   uint32_t keys[256];            // [0..43] round keys, [48..51] H (device-keyed contexts read these)
-  uint8_t htab[3][kByteTab];     // byte tables for H^1, H^2, H^4
-  uint8_t ntab[kNibTables][kNibTab];
+  uint8_t htab[3][kByteTab];     // byte tables for H^1, H^2, H^4 (lane groups' Horner multipliers)
   uint8_t ltab[66][16];          // OCB: L_*, L_$, L_0..L_63
   // device-keyed (602 sub-key) contexts: written by gcm_keysetup_kernel / gcm_tables_kernel
   uint8_t sqmat[31][128][16];    // columns of X -> X^(2^i), i = 1..31 (key independent, host)
   uint8_t h2pow[32][16];         // H^(2^i)
   uint8_t chains[10][128][16];   // basis chains of H, H^2, H^3, H^4, H^8, H^16, H^32, H^64, H^12, H^48
-  uint8_t h64[kByteTab];         // byte table of H^64 (wide plan)
-  uint8_t wnib[7][kNibTab];      // nibble tables of H^(2^b), b < 7 (wide plan)
-  uint8_t fnib[10][kNibTab];     // nibble tables of H^1,2,3,4,8,12,16,32,48,64 (gcm_flow_kernel)
+  // nibble tables of H^1,2,3,4,8,12,16,32,48,64: gcm_flow_kernel (all ten), lane-group weights
+  // H^1..H^3 (the first three)
+  uint8_t fnib[10][kNibTab];
 };
 
 // Columns of the squaring maps X -> X^(2^i) (key setup of device-derived keys), once per process.
@@ -143,9 +141,6 @@ struct cmpi_ctx {
   mutable hipEvent_t scratch_ev = nullptr;
   mutable bool scratch_used = false;
   mutable std::mutex smu;  // scratch lease (held through the launches of one call)
-  // arrival counters of the FLOW wide kernel's fused combine (zero between launches; ordered
-  // like the scratch: the same lease)
-  mutable uint32_t* wcnt = nullptr;
   mutable uint8_t* stage = nullptr;
   mutable size_t stage_cap = 0;
   mutable hipStream_t hstream = nullptr;
@@ -174,7 +169,6 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
   return CMPI_OK;
 }
 
-constexpr uint32_t kWideCounters = 16384;  // records of one fused-combine wide launch, at most
 // Workspace of one batch call: the caller's buffer, or the context's scratch under a lease that
 // holds the ctx lock through the launches, makes the launch stream wait for the scratch's previous
 // user and records the new last use when it ends (NULL-workspace calls from two
@@ -206,17 +200,6 @@ struct ScratchLease {
     ptr = (uint8_t*)c->scratch;
     return CMPI_OK;
   }
-  // the context's zeroed arrival counters (kWideCounters of them), allocated on first use
-  int counters(uint32_t** out) {
-    int rc = order();
-    if (rc) return rc;
-    if (!c->wcnt) {
-      HIP_TRY(hipMalloc(&c->wcnt, kWideCounters * 8 * sizeof(uint32_t)));  // per record: count, pad, 16-B accumulator
-      HIP_TRY(hipMemsetAsync(c->wcnt, 0, kWideCounters * 8 * sizeof(uint32_t), st));
-    }
-    *out = c->wcnt;
-    return CMPI_OK;
-  }
   ~ScratchLease() {
     if (internal && hipEventRecord(c->scratch_ev, st) == hipSuccess) c->scratch_used = true;
   }
@@ -241,28 +224,23 @@ constexpr uint64_t kWideFixedSteps = 4;
 struct GcmPlan {
   int L;
   uint32_t nb, nseg, G, r0;
-  bool wide = false;  // gcm_wide_kernel: nseg = chunks per record, G = 64*S X-blocks per chunk
+  bool wide = false;  // gcm_flow_kernel: nseg = chunks per record, G = 64*S X-blocks per chunk
   uint32_t S = 0;
-  uint32_t nt = 0;    // FLOW kernel threads per workgroup (0: g_flow_nt)
+  uint32_t nt = 1024; // FLOW kernel threads per workgroup
 };
 
-// test hook (include/cmpi_debug.h): force lanes-per-record / segments, 0 = automatic
-std::atomic<int> g_force_L{0};
-std::atomic<uint32_t> g_force_nseg{0};
-std::atomic<int> g_gcm_mem{0};        // lane kernel record-data cache policy: bit 0 nt loads, bit 1 nt stores
-std::atomic<int> g_gcm_pf{2};         // GCM input prefetch depth (slots), 2/3/4/6
-std::atomic<int> g_gcm_aw{0};         // GCM lane kernel: sector-aligned windows where legal (gcm_lane_kernel AW; opt-in)
-std::atomic<int> g_gcm_form{0};       // GCM lane plan: 0 gcm_lane_kernel, 1 the first form gcm_batch_kernel
-std::atomic<int> g_wide_chw{1};       // wide plan, host-keyed: barrier-free FLOW kernel with chunk weights (1) or weights in the combine (0)
-std::atomic<int> g_force_wide{0};     // wide decomposition: 0 automatic, 1 always (when legal), -1 never
-std::atomic<int> g_flow_nt{1024};     // FLOW wide kernel threads per workgroup (512 / 1024), 0 = round-1 kernel
-std::atomic<int> g_flow_one_wg{1};   // FLOW kernel: one-workgroup batches finish their tags in-kernel
-std::atomic<int> g_flow_fused{0};     // FLOW wide kernel flags: bit 0 combine fused, bits 1-3 timing ablations, bit 4 round-2-first form, bit 5 no automatic 512-thread workgroups
-std::atomic<uint32_t> g_force_S{0};   // wide steps per chunk, 0 = automatic
-std::atomic<int> g_ctr_lds{65536};
-std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics: wide-kernel phase timestamps
-std::atomic<int> g_sched{7 | 16384};  // wave priority: bit 0 GCM, bit 1 CTR, bit 2 OCB rotation; bit 14 GCM progress-based
-std::atomic<int> g_gcm_ablation{0};  // timing ablation of the L=4 seal kernel (tools/ablate.py)  // LDS requested by the CTR kernel (occupancy experiments)
+// test hooks (include/cmpi_debug.h): they pick among correct decompositions, never change output
+std::atomic<int> g_force_L{0};          // lanes per record, 0 = automatic
+std::atomic<uint32_t> g_force_nseg{0};  // segments per record, 0 = automatic
+std::atomic<int> g_force_wide{0};       // wide decomposition: 0 automatic, 1 always (when legal), -1 never
+std::atomic<uint32_t> g_force_S{0};     // wide steps per chunk, 0 = automatic
+std::atomic<int> g_flow_nt{0};          // FLOW kernel threads per workgroup: 0 automatic, 512 / 1024 forced
+std::atomic<int> g_flow_one_wg{1};      // FLOW kernel: one-workgroup batches finish their tags in-kernel
+#if CMPI_TOOLS
+std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics build: per-workgroup phase timestamps
+#endif
+// wave priority: bit 1 CTR, bit 2 OCB rotate per step (the GCM kernels: progress / rotation, fixed)
+constexpr uint32_t kSched = 7u;
 
 GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   GcmPlan p{};
@@ -282,9 +260,9 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   }
   if (g_force_L.load()) p.L = g_force_L.load();
   if (g_force_nseg.load()) nseg = std::min<uint64_t>(g_force_nseg.load(), nx);
-  // Wide decomposition when the lane-group plan leaves most of the chip idle (few long
-  // records: the naive collectives' p peer blocks).  Host-keyed contexts only (the chunk
-  // weights are built from H on the host); records need >= 64 data blocks.
+  // Wide decomposition (gcm_flow_kernel) when the lane-group plan leaves most of the chip idle
+  // (few long records: the naive collectives' p peer blocks, 602 segments, single messages);
+  // records need >= 64 data blocks.
   const int fw = g_force_wide.load();
   const bool wide_ok = p.nb >= 64;
   if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target &&
@@ -293,10 +271,9 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     // staging/weight phases) + S steps.  Chunks are cut from the end with chunk 0 absorbing the
     // remainder (G <= its length < 2G), so 1 MiB records (nx = 2^16 + 1) split into exactly
     // 2^16 / G chunks instead of one extra 1-block chunk that would start a second round.
-    // FLOW (host-keyed): 512-thread workgroups, one per CU (228 VGPRs, no spills; 8 x 1 MiB at S = 4:
-    // 22.6 us vs 30.9 at 1024 threads, tools/ab_flow.py); round-1 kernel: 1024 threads
-    const bool flow = !c->dev_keys && g_wide_chw.load() && g_flow_nt.load();
-    const uint64_t W = (uint64_t)c->ncu * (flow ? 8 : kGcmThreads / 64);
+    // 512-thread workgroups, one per CU (228 VGPRs, no spills; 8 x 1 MiB at S = 4: 22.6 us vs
+    // 30.9 at 1024 threads): a round is 8 waves per CU
+    const uint64_t W = (uint64_t)c->ncu * 8;
     const uint64_t smax = std::max<uint64_t>(1, nx / 64);
     uint64_t S = g_force_S.load();
     if (!S) {
@@ -309,7 +286,7 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
       }
     }
     S = std::min<uint64_t>(std::max<uint64_t>(S, 1), smax);
-    if (c->dev_keys) S = (uint64_t)1 << (63 - __builtin_clzll(S));  // chunk weights from H^(2^i)
+    if (c->dev_keys) S = (uint64_t)1 << (63 - __builtin_clzll(S));  // combine weights from H^(2^i)
     p.wide = true;
     p.S = (uint32_t)S;
     p.L = 64;
@@ -317,9 +294,9 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     p.nseg = (uint32_t)std::max<uint64_t>(1, nx / p.G);
     p.r0 = (uint32_t)(nx - (uint64_t)(p.nseg - 1) * p.G);
     // few waves (single messages, the 600/EVP regime; the naive alltoall's 8 x 1 MiB): 512-thread
-    // workgroups (1 x 64 KiB seal 21.0 -> 15.7 us at S = 2, tools/ab_flow.py)
-    if (g_flow_nt.load() == 1024 && !(g_flow_fused.load() & 32) && (uint64_t)nrec * p.nseg <= (uint64_t)c->ncu * 8)
-      p.nt = 512;
+    // workgroups (1 x 64 KiB seal 21.0 -> 15.7 us at S = 2)
+    if ((uint64_t)nrec * p.nseg <= (uint64_t)c->ncu * 8) p.nt = 512;
+    if (g_flow_nt.load()) p.nt = (uint32_t)g_flow_nt.load();
     return p;
   }
   uint64_t G = (nx + nseg - 1) / nseg;
@@ -337,18 +314,6 @@ size_t gcm_ws_bytes(const cmpi_ctx* c, const GcmPlan& p, size_t nrec) {
   if (p.wide) return (size_t)nrec * p.nseg * 16 + nrec * 16;  // (E_K(J0) slots double as statuses)
   if (p.nseg <= 1) return 0;
   return (size_t)nrec * p.nseg * 16 + nrec * 16;
-}
-
-// Byte table of H^64 (the wide kernel's Horner multiplier), built once per context.
-int get_h64tab(const cmpi_ctx* c, const u32x4** out) {
-  *out = reinterpret_cast<const u32x4*>(c->dt->h64);  // ctx_new (host key) / gcm_tables_kernel
-  return CMPI_OK;
-}
-
-// Lane weights of the wide kernel: nibble tables of H^(2^b), b = 0..6 (7 x 8 KiB).
-int get_wnib(const cmpi_ctx* c, const u32x4** out) {
-  *out = reinterpret_cast<const u32x4*>(c->dt->wnib[0]);
-  return CMPI_OK;
 }
 
 // Combine multipliers M_j = H^{G·2^j}, j < 7 (gcm_combine_kernel).  Host-keyed contexts: computed
@@ -447,48 +412,7 @@ int launch_gcm_combine(const cmpi_ctx* c, cmpi::dev::GcmCombineArgs& ca, uint32_
 
 template <int L, bool DEC>
 int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
-  // default: the round-2 lane kernel; the first form stays behind the A/B / ablation knobs
-  const bool first_form = g_gcm_form.load() == 1 || g_gcm_pf.load() != 2 || g_gcm_mem.load() != 0 ||
-                          (!DEC && g_gcm_ablation.load() != 0 && g_gcm_ablation.load() < 16) || (a.sched & 8192u);
-  // sector-aligned windows (gcm_lane_kernel AW): 16-B-aligned records, one segment, nrec % 64 == 0
-  const bool aw = L == 4 && g_gcm_aw.load() && a.nseg == 1 && a.nrec % 64u == 0 &&
-                  ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.out) | a.in_stride | a.out_stride) & 15u) == 0;
-  auto fn = first_form ? cmpi::dev::gcm_batch_kernel<L, DEC>
-                       : aw ? cmpi::dev::gcm_lane_kernel<L, DEC, 1, 0, true> : cmpi::dev::gcm_lane_kernel<L, DEC>;
-  if constexpr (!DEC) {  // ablations of the round-2 form (tools/ablate_split.py): 16 no memory, 32 no AES
-    switch (g_gcm_ablation.load()) {
-      case 16: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 1>; break;
-      case 32: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 2>; break;
-      case 48: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 3>; break;
-      case 64 + 16: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 5>; break;  // AES only
-      case 64 + 32: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 6>; break;  // memory only
-      case 64: fn = cmpi::dev::gcm_lane_kernel<L, DEC, 1, 4>; break;
-      default: break;
-    }
-  }
-  switch (g_gcm_pf.load()) {
-    case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 3>; break;
-    case 4: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 4>; break;
-    case 6: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 6>; break;
-    default: break;
-  }
-  switch (g_gcm_mem.load()) {  // non-temporal record loads (1) / stores (2) / both (3)
-    case 1: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 2, 1>; break;
-    case 2: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 2, 2>; break;
-    case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 0, 2, 3>; break;
-    default: break;
-  }
-  if constexpr (!DEC) {
-    switch (g_gcm_ablation.load()) {
-      case 1: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 1>; break;
-      case 2: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 2>; break;
-      case 3: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 3>; break;
-      case 4: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 4>; break;
-      case 7: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 7>; break;
-      case 8: fn = cmpi::dev::gcm_batch_kernel<L, DEC, 8>; break;
-      default: break;
-    }
-  }
+  auto fn = cmpi::dev::gcm_lane_kernel<L, DEC>;
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), device, lds);
   if (rc) return rc;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
@@ -537,7 +461,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.r0 = p.r0;
   a.ngroups = (uint32_t)(nrec * p.nseg);
   a.htab = reinterpret_cast<const u32x4*>(c->dt->htab[p.L == 1 ? 0 : (p.L == 2 ? 1 : 2)]);
-  a.ntab = reinterpret_cast<const u32x4*>(c->dt->ntab[0]);
+  a.ntab = reinterpret_cast<const u32x4*>(c->dt->fnib[0]);  // H^1..H^3
   a.te0 = c->dt->te0;
   a.status = status;
   a.rk = folded(c->rk);
@@ -548,7 +472,9 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.nflag2 = ns.flag2;
   a.nflag2_from = ns.flag2_from;
   memcpy(a.nfix, ns.fix, sizeof a.nfix);
-  a.sched = (uint32_t)g_sched.load();
+#if CMPI_TOOLS
+  a.probe = g_wide_probe.load();
+#endif
   ScratchLease lease(c, workspace, st);
   if (p.wide) {
     if ((uint64_t)nrec * p.nseg * 16 > 0xFFFFFFFFull) return fail(CMPI_EINVAL, "too many chunks");
@@ -559,10 +485,9 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
     a.S = p.S;
     a.nch = p.nseg;
-    int rc = get_h64tab(c, &a.htab);
-    if (!rc) rc = get_wnib(c, &a.wtab);
+    a.wtab = reinterpret_cast<const u32x4*>(c->dt->fnib[0]);
     bool chw_transient = false;
-    if (!rc && g_wide_chw.load() && !(a.sched & 8u)) rc = get_chw(c, p.G, p.nseg, &a.chw, st, &chw_transient);
+    int rc = get_chw(c, p.G, p.nseg, &a.chw, st, &chw_transient);  // null for device-keyed contexts
     if (rc) return rc;
     // a transient weights buffer is released in stream order after this call's launches
     struct FreeAsync {
@@ -572,56 +497,25 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
         if (p) (void)hipFreeAsync(const_cast<void*>(p), s);
       }
     } chw_guard{chw_transient ? (const void*)a.chw : nullptr, st};
-    a.probe = g_wide_probe.load();
     const uint64_t waves = (uint64_t)nrec * p.nseg;
-    if (a.chw && g_flow_nt.load()) {
-      // FLOW kernel: NT threads per workgroup; radix-4 form unless disabled (flags bit 4);
-      // combine fused (counters + accumulators in the context's zeroed scratch) unless disabled
-      const int NT = p.nt ? (int)p.nt : g_flow_nt.load();
-      const int flags = g_flow_fused.load();
-      const bool r4 = !(flags & 16);
-      // every chunk of the batch in one workgroup (single small messages): the tags are finished
-      // from the workgroup's LDS aggregation in the same launch (cmpi_debug_set_flow_one_wg: A/B)
-      const bool one_wg = r4 && g_flow_one_wg.load() && waves <= (uint64_t)(NT / 64);
-      const bool fused = one_wg || ((flags & 1) && nrec <= kWideCounters);
-      a.one_wg = one_wg ? 1u : 0u;
-      if (fused) {
-        if (!one_wg && (rc = lease.counters(&a.wcnt))) return rc;
-        if (DEC && !status) {  // the verdicts go somewhere: the tail of the partials buffer
-          a.status = reinterpret_cast<int32_t*>(ws + (size_t)nrec * p.nseg * 16);
-        }
-      }
-      a.sched |= (uint32_t)((flags >> 1) & 7) << 8;  // timing ablations (cmpi_debug_set_flow)
-      a.sched |= (uint32_t)((flags >> 7) & 3) << 11;  // bits 7-8: no stores / no loads (ablations)
-      a.wtab = r4 ? reinterpret_cast<const u32x4*>(c->dt->fnib[0]) : a.wtab;
-      const void* fn;
-      if (r4) fn = NT == 512 ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, true>)
-                             : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, true>);
-      else fn = NT == 512 ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, false>)
-                          : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, false>);
-      const size_t lds = r4 ? (size_t)cmpi::dev::kFlowLdsR4 : (size_t)cmpi::dev::kGcmNib + 4 * 8192;
-      if ((rc = set_lds_attr(fn, c->device, lds))) return rc;
-      const uint32_t wpb = (uint32_t)NT / 64u;
-      const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + wpb - 1) / wpb, (uint64_t)c->ncu));
-      void* kargs[] = {&a};
-      HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(NT), kargs, lds, st));
-      if (fused) {
-        if (DEC && !one_wg) {  // zero-fill failed records after the launch (gcm_flow_kernel: cross-XCD L2s)
-          hipLaunchKernelGGL(cmpi::dev::zero_failed_kernel, dim3((uint32_t)nrec), dim3(256), 0, st, out,
-                             (uint64_t)out_stride, (uint32_t)len, (const int32_t*)a.status);
-          HIP_TRY(hipGetLastError());
-        }
-        return CMPI_OK;
-      }
-    } else {
-      auto fn = a.chw ? cmpi::dev::gcm_wide_kernel<DEC, true> : cmpi::dev::gcm_wide_kernel<DEC, false>;
-      const size_t lds = a.chw ? (size_t)cmpi::dev::kGcmNib + 4 * 8192 : 2 * 65536;
-      if ((rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds))) return rc;
-      const uint32_t grid = (uint32_t)std::max<uint64_t>(
-          1, std::min<uint64_t>((waves + kGcmThreads / 64 - 1) / (kGcmThreads / 64), (uint64_t)c->ncu));
-      hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
-      HIP_TRY(hipGetLastError());
-    }
+    const int NT = (int)p.nt;
+    // every chunk of the batch in one workgroup (single small messages, host-keyed): the tags are
+    // finished from the workgroup's LDS aggregation in the same launch
+    const bool one_wg = a.chw && g_flow_one_wg.load() && waves <= (uint64_t)(NT / 64);
+    a.one_wg = one_wg ? 1u : 0u;
+    if (one_wg && DEC && !status) a.status = reinterpret_cast<int32_t*>(ws + (size_t)nrec * p.nseg * 16);
+    const bool dk = !a.chw;  // device-keyed context
+    const void* fn = NT == 512 ? (dk ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, true>)
+                                     : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, false>))
+                               : (dk ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, true>)
+                                     : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, false>));
+    const size_t lds = (size_t)cmpi::dev::kFlowLds;
+    if ((rc = set_lds_attr(fn, c->device, lds))) return rc;
+    const uint32_t wpb = (uint32_t)NT / 64u;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + wpb - 1) / wpb, (uint64_t)c->ncu));
+    void* kargs[] = {&a};
+    HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(NT), kargs, lds, st));
+    if (one_wg) return CMPI_OK;
     cmpi::dev::GcmCombineArgs ca{};
     ca.in = in;
     ca.out = out;
@@ -632,7 +526,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     ca.nrec = (uint32_t)nrec;
     ca.nseg = p.nseg;
     ca.partial = a.partial;
-    ca.ekj0 = a.chw ? nullptr : a.ekj0;
+    ca.ekj0 = a.chw ? nullptr : a.ekj0;  // device-keyed: E_K(J0) and the chunk weights applied here
     ca.status = status;
     ca.prew = a.chw ? 1u : 0u;
     return launch_gcm_combine<DEC>(c, ca, p.G, st);  // chunk i weighted by H^{(nch-1-i)·64S}, as segments
@@ -645,7 +539,6 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
   }
   const size_t lds = cmpi::dev::gcm_lds_bytes(p.L);
-  a.probe = g_wide_probe.load();
   const uint64_t want = ((uint64_t)a.ngroups * p.L + kGcmThreads - 1) / kGcmThreads;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->ncu));
   int rc;
@@ -755,7 +648,7 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.off0 = d_off0;
   a.partial = d_part;
   a.rk = folded(c->rk);
-  a.sched = (uint32_t)g_sched.load();
+  a.sched = kSched;
   a.drk = folded(c->drk);
   const size_t lds = DEC ? cmpi::dev::kOcbLdsOpen : cmpi::dev::kOcbLdsSeal;
   const uint32_t per_cu = DEC ? 1u : 2u;  // LDS-limited 1024-thread blocks per CU
@@ -1128,12 +1021,12 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   a.ctr_lo = cmpi::be64(ctr + 8);
   a.te0 = c->dt->te0;
   a.rk = folded(c->rk);
-  a.sched = (uint32_t)g_sched.load();
+  a.sched = kSched;
   const uint64_t blocks = (a.nblk + 1023) / 1024;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 2));
   hipStream_t st = (hipStream_t)stream;
   auto fn = in ? cmpi::dev::ctr_kernel<true> : cmpi::dev::ctr_kernel<false>;
-  const int lds = g_ctr_lds.load();
+  const int lds = 65536;
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds);
   if (rc) return rc;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(1024), lds, st, a);
@@ -1239,19 +1132,10 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
     }
   }
   if (alg == CMPI_AES_128_GCM) {
-    const Blk H2 = cmpi::gf_mul(c->H, c->H), H3 = cmpi::gf_mul(H2, c->H), H4 = cmpi::gf_mul(H2, H2);
+    const Blk H2 = cmpi::gf_mul(c->H, c->H), H4 = cmpi::gf_mul(H2, H2);
     cmpi::build_byte_table(c->H, reinterpret_cast<Blk*>(ht->htab[0]));
     cmpi::build_byte_table(H2, reinterpret_cast<Blk*>(ht->htab[1]));
     cmpi::build_byte_table(H4, reinterpret_cast<Blk*>(ht->htab[2]));
-    const Blk pw[4] = {c->H, H2, H3, H4};
-    for (int i = 0; i < 4; ++i) cmpi::build_nibble_table(pw[i], reinterpret_cast<Blk*>(ht->ntab[i]));
-    // wide plan: byte table of H^64, nibble tables of H^(2^b), b < 7
-    Blk p = c->H;
-    for (int b = 0; b < 7; ++b) {
-      cmpi::build_nibble_table(p, reinterpret_cast<Blk*>(ht->wnib[b]));
-      if (b == 6) cmpi::build_byte_table(p, reinterpret_cast<Blk*>(ht->h64));  // p = H^64
-      p = cmpi::gf_mul(p, p);
-    }
     for (uint32_t f = 0; f < cmpi::dev::kFlowNib; ++f)
       cmpi::build_nibble_table(cmpi::gf_pow(c->H, cmpi::dev::flow_nib_exp(f)), reinterpret_cast<Blk*>(ht->fnib[f]));
   }
@@ -1295,7 +1179,6 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   if (c->scratch_used) (void)hipEventSynchronize(c->scratch_ev);
   if (c->scratch_ev) (void)hipEventDestroy(c->scratch_ev);
   if (c->scratch) (void)hipFree(c->scratch);
-  if (c->wcnt) (void)hipFree(c->wcnt);
   for (auto& kv : c->chw) (void)hipFree(kv.second);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
@@ -1333,29 +1216,18 @@ int cmpi_host_unregister(void* ptr) {
   return CMPI_OK;
 }
 
-void cmpi_debug_set_sched(int mode) { g_sched.store(mode & (7 | 4096 | 8192 | 16384 | 32768)); }
 void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)16 << 20)); }
-void cmpi_debug_set_gcm_ablation(int mode) { g_gcm_ablation.store(mode & 127); }
-
-void cmpi_debug_set_ctr_lds(int lds_bytes) {
-  g_ctr_lds.store(lds_bytes >= 65536 && lds_bytes <= 163840 ? lds_bytes : 65536);
-}
 
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
   g_force_L.store(lanes_per_record == 1 || lanes_per_record == 2 || lanes_per_record == 4 ? lanes_per_record : 0);
   g_force_nseg.store(segments);
 }
 
-void cmpi_debug_set_wide_chw(int on) { g_wide_chw.store(on ? 1 : 0); }
 void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
-void cmpi_debug_set_gcm_mem(int mode) { g_gcm_mem.store(mode & 3); }
 void cmpi_debug_set_host_spin(int on) { g_host_spin.store(on ? 1 : 0); }
 
 void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }
-void cmpi_debug_set_flow(int threads, int fused) {
-  g_flow_nt.store(threads == 512 || threads == 1024 ? threads : (threads == 0 ? 0 : 1024));
-  g_flow_fused.store(fused);  // bit 0 fused combine; bits 1-3 timing ablations (wrong output); bit 4 !R4
-}
+void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 || threads == 1024 ? threads : 0); }
 
 // Timing events without the system-scope release fence (hipEventDisableSystemFence): a default
 // event's fence writes back and invalidates the caches and leaves a ~6 us bubble before the
@@ -1376,13 +1248,9 @@ float cmpi_debug_event_ms(void* a, void* b) {
 void cmpi_debug_event_free(void* ev) {
   if (ev) (void)hipEventDestroy((hipEvent_t)ev);
 }
+#if CMPI_TOOLS
 void cmpi_debug_set_wide_probe(void* buf) { g_wide_probe.store(reinterpret_cast<uint64_t*>(buf)); }
-
-void cmpi_debug_set_gcm_form(int form) {
-  g_gcm_form.store(form == 1 ? 1 : 0);
-  g_gcm_aw.store(form == 3 ? 1 : 0);
-}
-void cmpi_debug_set_gcm_prefetch(int slots) { g_gcm_pf.store(slots == 3 || slots == 4 || slots == 6 ? slots : 2); }
+#endif
 
 void cmpi_debug_force_wide(int mode, uint32_t steps) {
   g_force_wide.store(mode > 0 ? 1 : (mode < 0 ? -1 : 0));
@@ -1580,9 +1448,6 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   cmpi::dev::TablesArgs ta{};
   ta.chains = a.chains;
   ta.htab = reinterpret_cast<u32x4*>(dst->dt->htab[0]);
-  ta.h64 = reinterpret_cast<u32x4*>(dst->dt->h64);
-  ta.ntab = reinterpret_cast<u32x4*>(dst->dt->ntab[0]);
-  ta.wnib = reinterpret_cast<u32x4*>(dst->dt->wnib[0]);
   ta.fnib = reinterpret_cast<u32x4*>(dst->dt->fnib[0]);
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_keysetup_kernel), dst->device, cmpi::dev::kKsLds);
   if (rc) return rc;
@@ -1635,9 +1500,6 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
   cmpi::dev::TablesArgs ta{};
   ta.chains = a.chains;
   ta.htab = reinterpret_cast<u32x4*>(c->dt->htab[0]);
-  ta.h64 = reinterpret_cast<u32x4*>(c->dt->h64);
-  ta.ntab = reinterpret_cast<u32x4*>(c->dt->ntab[0]);
-  ta.wnib = reinterpret_cast<u32x4*>(c->dt->wnib[0]);
   ta.fnib = reinterpret_cast<u32x4*>(c->dt->fnib[0]);
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_keysetup_kernel), c->device, cmpi::dev::kKsLds);
   if (rc) return rc;

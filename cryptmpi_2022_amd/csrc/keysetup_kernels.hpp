@@ -4,10 +4,9 @@
 // expanded and tabled without a host round trip, ordered on the caller's stream.
 //
 // Output layout = DevTables in cmpi_aead.hip: keys[0..43] round keys (folded), keys[48..51] H,
-// H^(2^i), basis chains; then gcm_tables_kernel expands byte tables of H, H^2, H^4, H^64
-// ([v][p], 4096 x 16 B each) and nibble tables of H^1..H^4 and H^(2^b) (512 x 16 B each) —
-// and the FLOW kernel's nibble tables of H^1,2,3,4,8,12,16,32,48,64 — bit-identical to
-// gf128_host.hpp's host builders.  Two launches, ~10 us in all.
+// H^(2^i), basis chains; then gcm_tables_kernel expands byte tables of H, H^2, H^4 ([v][p],
+// 4096 x 16 B each) and the nibble tables of H^1,2,3,4,8,12,16,32,48,64 (512 x 16 B each) —
+// bit-identical to gf128_host.hpp's host builders.  Two launches.
 #pragma once
 #include "aes_device.hpp"
 
@@ -143,18 +142,16 @@ __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
 // Table expansion, one entry per thread (grid over every entry): entry (v, p) of a byte table
 // of P = XOR over set bits k of v of P · x^(8p + 7 - k); nibble entry (2p + h, v) likewise over
 // the 4 bits of v at x^(8p + 7 - k - (h ? 0 : 4)).  Outputs: byte tables of H, H^2, H^4 (GCM
-// lane groups) and H^64 (wide), nibble tables of H^1..H^4 and of H^(2^b), b = 0..6 (wide).
+// lane groups' Horner multipliers) and the ten nibble tables of H^1,2,3,4,8,12,16,32,48,64
+// (gcm_flow_kernel; the lane groups' weights H^1..H^3 are the first three).
 struct TablesArgs {
-  const u32x4* chains;  // 8 x 128 (ks_chain_exp order)
+  const u32x4* chains;  // 10 x 128 (ks_chain_exp order)
   u32x4* htab;          // 3 x 4096: H, H^2, H^4
-  u32x4* h64;           // 4096
-  u32x4* ntab;          // 4 x 512: H^1..H^4
-  u32x4* wnib;          // 7 x 512: H^(2^b)
-  u32x4* fnib;          // 10 x 512: H^1, 2, 3, 4, 8, 12, 16, 32, 48, 64 (gcm_flow_kernel, radix-4 tree)
+  u32x4* fnib;          // 10 x 512: H^1, 2, 3, 4, 8, 12, 16, 32, 48, 64
 };
 constexpr uint32_t kFlowNib = 10;
-constexpr uint32_t kTabEntries = 4u * 4096u + (11u + kFlowNib) * 512u;
-// exponent of H of FLOW nibble table f, and its basis chain
+constexpr uint32_t kTabEntries = 3u * 4096u + kFlowNib * 512u;
+// exponent of H of nibble table f, and its basis chain
 __host__ __device__ constexpr uint32_t flow_nib_exp(uint32_t f) {
   return f == 0 ? 1u : f == 1 ? 2u : f == 2 ? 3u : f == 3 ? 4u : f == 4 ? 8u : f == 5 ? 12u : f == 6 ? 16u
        : f == 7 ? 32u : f == 8 ? 48u : 64u;
@@ -166,32 +163,26 @@ __host__ __device__ constexpr uint32_t flow_nib_chain(uint32_t f) {
 __global__ __launch_bounds__(256) void gcm_tables_kernel(TablesArgs a) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= kTabEntries) return;
-  // byte tables: 0..3 -> chain 0 (H), 1 (H^2), 3 (H^4), 7 (H^64)
-  if (e < 4u * 4096u) {
+  // byte tables: 0..2 -> chain 0 (H), 1 (H^2), 3 (H^4)
+  if (e < 3u * 4096u) {
     const uint32_t t = e >> 12, v = (e >> 4) & 255u, p = e & 15u;
-    const uint32_t ch = t == 0 ? 0u : t == 1 ? 1u : t == 2 ? 3u : 7u;
+    const uint32_t ch = t == 0 ? 0u : t == 1 ? 1u : 3u;
     const u32x4* c = a.chains + ch * 128u + 8u * p + 7u;
     u32x4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       if (v & (1u << k)) acc ^= *(c - k);
-    if (t < 3u) a.htab[e] = acc;
-    else a.h64[e - 3u * 4096u] = acc;
+    a.htab[e] = acc;
     return;
   }
-  // nibble tables: 0..3 -> H^1..H^4 (chains 0..3); 4..10 -> H^(2^b) (chains 0, 1, 3, 4, 5, 6, 7)
-  const uint32_t f = e - 4u * 4096u;
+  const uint32_t f = e - 3u * 4096u;
   const uint32_t t = f >> 9, row = (f >> 4) & 31u, v = f & 15u, p = row >> 1, sh = (row & 1u) ? 0u : 4u;
-  const uint32_t b = t - 4u;
-  const uint32_t ch = t < 4u ? t : t >= 11u ? flow_nib_chain(t - 11u) : (b == 0u ? 0u : b == 1u ? 1u : b + 1u);
-  const u32x4* c = a.chains + ch * 128u + 8u * p + 7u - sh;
+  const u32x4* c = a.chains + flow_nib_chain(t) * 128u + 8u * p + 7u - sh;
   u32x4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     if (v & (1u << k)) acc ^= *(c - k);
-  if (t < 4u) a.ntab[f] = acc;
-  else if (t < 11u) a.wnib[f - 4u * 512u] = acc;
-  else a.fnib[f - 11u * 512u] = acc;
+  a.fnib[f] = acc;
 }
 
 }  // namespace dev

@@ -28,8 +28,7 @@ def _auto_plan():
     yield
     aead.force_plan(0, 0)
     aead.force_wide(0, 0)
-    aead.set_wide_chw(True)
-    aead.set_flow(1024, 0)
+    aead.set_flow_threads(0)
     aead.set_flow_one_wg(True)
     aead.N.lib().cmpi_debug_set_host_direct(DIRECT_DEFAULT)
 
@@ -189,14 +188,14 @@ def test_large_records_multisegment():
 
 @pytest.mark.parametrize("n,nrec,steps", [(1024, 3, 1), (1040, 2, 1), (4097, 3, 2), (65535, 2, 4), (100000, 3, 3),
                                           (1 << 20, 2, 0), (64 * 16 * 5 - 16, 2, 5)])
-@pytest.mark.parametrize("chw", [True, False])
-def test_wide_decomposition(n, nrec, steps, chw):
-    """Wide plan (one wave per 64*steps-block chunk; chunk 0 takes the remainder, G <= r0 < 2G
-    or the whole record; lane-weighted partials; chunk weights applied in the wide kernel by a
-    wave-cooperative multiply, or by the combine kernel): bit-exact seal, round trip, forged
-    record zero-filled, unaligned wire layout."""
+@pytest.mark.parametrize("one_wg", [True, False])
+def test_wide_decomposition(n, nrec, steps, one_wg):
+    """Wide plan (gcm_flow_kernel: one wave per 64*steps-block chunk; chunk 0 takes the remainder,
+    G <= r0 < 2G or the whole record; radix-4 lane tree; chunk weights applied in the kernel by a
+    wave-cooperative multiply, partials XOR-combined in the same launch or by the combine
+    launch): bit-exact seal, round trip, forged record zero-filled, unaligned wire layout."""
     aead.force_wide(1, steps)
-    aead.set_wide_chw(chw)
+    aead.set_flow_one_wg(one_wg)
     ctx = aead.AeadCtx(KEY)
     L, nch, G, r0 = aead.gcm_plan(ctx, n, nrec)
     nx = n // 16 + (n % 16 > 0) + 1
@@ -220,19 +219,14 @@ def test_wide_decomposition(n, nrec, steps, chw):
     assert np.array_equal(host(wbuf).reshape(nrec, stride)[:, 12:], want)
 
 
-@pytest.mark.parametrize("threads,flags", [(1024, 0), (512, 32), (1024, 32), (1024, 1), (512, 33), (1024, 16),
-                                           (1024, 17), (1024, 48), (1024, 49)])
+@pytest.mark.parametrize("threads", [1024, 512])
 @pytest.mark.parametrize("n,nrec,steps", [(64 * 16 * 3 - 16, 11, 1), (4097, 5, 2), (1 << 20, 2, 0)])
-def test_flow_kernel_forms(threads, flags, n, nrec, steps):
-    """gcm_flow_kernel in each form — radix-4 tree (nibble tables H^1..H^64, one chunk-weight
-    product) or the round-2 first form (byte-table Horner, radix-2 tree, 4 products); 512 or 1024
-    threads; partials combined by gcm_xor_combine_kernel or fused (per-workgroup XOR then 8-B agent
-    atomics into the record's accumulator, last adder writes the tag).  3-chunk records put up to
-    six records in one workgroup.  Two seals back to back (the fused counters and accumulators
-    must return to zero), a forged record, and a context re-keyed on the device (tables rebuilt
-    by gcm_tables_kernel, bit-identical to the host build)."""
+def test_flow_kernel_forms(threads, n, nrec, steps):
+    """gcm_flow_kernel at 512 and 1024 threads per workgroup; 3-chunk records put up to six
+    records in one workgroup.  Two seals back to back, a forged record, and a context re-keyed
+    on the device (tables rebuilt by gcm_tables_kernel, bit-identical to the host build)."""
     aead.force_wide(1, steps)
-    aead.set_flow(threads, flags)
+    aead.set_flow_threads(threads)
     key2 = bytes(range(100, 116))
     ctx = aead.AeadCtx(KEY)
     pt = records(0x5100 + n, nrec, n)
@@ -260,7 +254,7 @@ def test_flow_one_workgroup(one_wg, threads, n, nrec, steps):
     Shapes on both sides of the 8 / 16 units-per-workgroup edge, seal twice, forged first and
     last records, then a clean open."""
     aead.force_wide(1, steps)
-    aead.set_flow(threads, 32)
+    aead.set_flow_threads(threads)
     aead.set_flow_one_wg(one_wg)
     ctx = aead.AeadCtx(KEY)
     pt = records(0x7100 + n, nrec, n)
@@ -278,86 +272,6 @@ def test_flow_one_workgroup(one_wg, threads, n, nrec, steps):
         assert (not back[i].any()) if i in bad else np.array_equal(back[i], pt[i])
     back, st = gpu_open(ctx, nonces, want)
     assert list(st) == [1] * nrec and np.array_equal(back, pt)
-
-
-@pytest.mark.parametrize("n", [0, 15, 16, 1000, 1024, 4096, 4097])
-@pytest.mark.parametrize("plan", [(4, 1), (2, 1), (4, 3), (1, 1)])
-@pytest.mark.parametrize("stride_pad", [0, 28])
-def test_output_aligned_windows(n, plan, stride_pad):
-    """Lane kernel with output-aligned windows (cmpi_debug_set_sched bit 13): lanes of a record
-    start phase-shifted so each step's stores fill whole 16L-byte sectors, and a seal holds the
-    tag window's data blocks back to store them with the tag.  Bit-exact seal (dense and wire
-    strides, where every record has its own phase), open, forged record zero-filled."""
-    L = aead.N.lib()
-    L.cmpi_debug_set_sched(7 | 8192)
-    try:
-        aead.force_plan(*plan)
-        nrec = 37
-        pt = records(0x6600 + n, nrec, n)
-        nonces = random_nonces(0x6700 + n, nrec)
-        ctx = aead.AeadCtx(KEY)
-        want = oracle.gcm_seal_batch(KEY, nonces, pt)
-        stride = n + 16 + stride_pad
-        out = empty(nrec * stride, fill=0xAA)
-        ctx.seal_batch(out, dev(pt), dev(nonces), n, nrec, out_stride=stride)
-        got = host(out)[: nrec * stride].reshape(nrec, stride)
-        assert np.array_equal(got[:, : n + 16], want) and (got[:, n + 16:] == 0xAA).all()
-        forged = want.copy()
-        forged[5, n // 2 if n else n + 3] ^= 1
-        back, st = gpu_open(ctx, nonces, forged)
-        assert st[5] == 0 and not back[5].any() and (np.delete(st, 5) == 1).all()
-        assert np.array_equal(np.delete(back, 5, axis=0), np.delete(pt, 5, axis=0))
-    finally:
-        L.cmpi_debug_set_sched(7 | 16384)
-
-
-def _strided(rows: np.ndarray, off: int, stride: int, fill: int) -> np.ndarray:
-    nrec, n = rows.shape
-    buf = np.full(off + nrec * stride, fill, np.uint8)
-    view = np.lib.stride_tricks.as_strided(buf[off:], shape=(nrec, n), strides=(stride, 1), writeable=True)
-    view[:] = rows
-    return buf
-
-
-@pytest.mark.parametrize("n", [0, 15, 16, 100, 1000, 1024, 1040, 4096, 4097])
-@pytest.mark.parametrize("in_off,in_pad,out_pad", [(0, 0, 0), (16, 16, 0), (48, 16, 32), (32, 0, 16)])
-@pytest.mark.parametrize("form", [3, 0])
-def test_sector_aligned_windows(n, in_off, in_pad, out_pad, form):
-    """Lane kernel with sector-aligned windows (L = 4, one segment, nrec % 64 == 0, 16-B-aligned
-    records; form 3 = opt-in, form 0 = the default kernel without them): records at every 16-B phase
-    on both sides (strides of odd and even block counts, input base offsets), DPP quad rotation of
-    the loaded blocks, records dealt to waves by residue mod 4.  Seal and open bit-exact vs the
-    oracle, gaps between records untouched, a forged record zero-filled."""
-    L = aead.N.lib()
-    L.cmpi_debug_set_gcm_form(form)
-    try:
-        aead.force_plan(4, 1)
-        nrec = 128
-        r16 = lambda x: (x + 15) // 16 * 16  # noqa: E731
-        pt = records(0x7100 + n, nrec, n)
-        nonces = random_nonces(0x7200 + n, nrec)
-        ctx = aead.AeadCtx(KEY)
-        want = oracle.gcm_seal_batch(KEY, nonces, pt)
-        in_stride, out_stride = r16(n) + in_pad, r16(n + 16) + out_pad
-        d_in = dev(_strided(pt, in_off, in_stride, 0x55))
-        out = empty(nrec * out_stride, fill=0xAA)
-        ctx.seal_batch(out, d_in[in_off:], dev(nonces), n, nrec, in_stride=in_stride, out_stride=out_stride)
-        got = host(out)[: nrec * out_stride].reshape(nrec, out_stride)
-        assert np.array_equal(got[:, : n + 16], want) and (got[:, n + 16:] == 0xAA).all()
-        forged = want.copy()
-        forged[5, n // 2 if n else n + 3] ^= 1
-        ct_stride, pt_stride = r16(n + 16) + in_pad, r16(n) + out_pad
-        d_ct = dev(_strided(forged, in_off, ct_stride, 0x33))
-        back = empty(nrec * pt_stride, fill=0xAA)
-        st = status_buf(nrec)
-        ctx.open_batch(back, d_ct[in_off:], dev(nonces), n, nrec, status=st, in_stride=ct_stride, out_stride=pt_stride)
-        b = host(back)[: nrec * pt_stride].reshape(nrec, pt_stride)
-        st = host(st)[:nrec]
-        assert st[5] == 0 and not b[5, :n].any() and (np.delete(st, 5) == 1).all()
-        assert np.array_equal(np.delete(b[:, :n], 5, axis=0), np.delete(pt, 5, axis=0))
-        assert (b[:, n:] == 0xAA).all()
-    finally:
-        L.cmpi_debug_set_gcm_form(0)
 
 
 @pytest.mark.parametrize("nrec,segments", [(3, 0), (2, 700), (1, 2)])
@@ -540,9 +454,10 @@ def test_derived_subkey_device_keyed(n, nrec, plan):
 @pytest.mark.parametrize("n,nrec,wide,plan", [(100000, 3, (1, 2), None), (1 << 20, 2, (1, 0), None),
                                            (65536, 9, (-1, 0), (4, 40)), (4097, 5, (-1, 0), (2, 3))])
 def test_derived_subkey_wide_and_pow2_segments(n, nrec, wide, plan):
-    """Device-keyed contexts on the wide plan (H^64 byte table and H^(2^b) nibble tables built
-    by the table kernel) and on multi-segment lane groups (G rounded to a power of two, combine
-    weights as products of H^(2^i)): bit-exact vs the oracle under K' = AES_K(V), forgery."""
+    """Device-keyed contexts on the wide plan (gcm_flow_kernel with the table kernel's nibble
+    tables; chunk weights as products of H^(2^i) in gcm_combine_kernel) and on multi-segment lane
+    groups (G rounded to a power of two, same combine): bit-exact vs the oracle under
+    K' = AES_K(V), forgery."""
     base = aead.CipherCtx(KEY, "aes-128-ecb")
     v = splitmix64_bytes(0x61200 + n, 16).tobytes()
     kprime = oracle.ecb_encrypt(KEY, v)
@@ -675,3 +590,35 @@ def test_config5_shape_default_plan(nrec, n):
     back, st = gpu_open(ctx, nonces, forged)
     assert list(st) == [1] * (nrec - 1) + [0]
     assert np.array_equal(back[: nrec - 1], pt[: nrec - 1]) and not back[nrec - 1].any()
+
+
+@pytest.mark.parametrize("n,nrec", [(32768, 16), (1 << 20, 8), (100000, 3), (65536 + 1, 1), (8 << 20, 1),
+                                    (64 * 16 * 3 - 5, 7)])
+@pytest.mark.parametrize("threads", [0, 1024])
+def test_derived_subkey_flow_plan(n, nrec, threads):
+    """602 per-message sub-key contexts (send.c:572-600: K' = AES_K(V) derived on the device) on
+    the planner's default flow plan at 602 shapes — OpenMP segments of 32 KiB, 1 MiB, single
+    messages just over 64 KiB and of 8 MiB: gcm_flow_kernel<DK> (round keys from HBM, partials
+    V·H) + gcm_combine_kernel (chunk weights from H^(2^i), E_K(J0)).  Seal and open bit-exact vs the
+    oracle under K', a forged record zero-filled, the context re-keyed to a second V."""
+    aead.set_flow_threads(threads)
+    base = aead.CipherCtx(KEY, "aes-128-ecb")
+    sub = None
+    for m, seed in enumerate((0x60600, 0x60601)):
+        v = splitmix64_bytes(seed + n, 16).tobytes()
+        kprime = oracle.ecb_encrypt(KEY, v)
+        if sub is None:
+            sub = aead.AeadCtx.derive_subkey(base, v)
+        else:
+            sub.rekey_subkey(base, v)
+        assert aead.gcm_plan(sub, n, nrec)[0] == 64, aead.gcm_plan(sub, n, nrec)
+        pt = records(0x6060 + n + m, nrec, n)
+        nonces = np.stack([np.frombuffer(oracle.nonce602(b"1" if i == nrec - 1 else b"0", i), np.uint8)
+                           for i in range(nrec)])
+        want = oracle.gcm_seal_batch(kprime, nonces, pt)
+        assert np.array_equal(gpu_seal(sub, nonces, pt), want), aead.gcm_plan(sub, n, nrec)
+        forged = want.copy()
+        forged[nrec - 1, n // 2] ^= 0x08
+        back, st = gpu_open(sub, nonces, forged)
+        assert list(st) == [1] * (nrec - 1) + [0]
+        assert np.array_equal(back[: nrec - 1], pt[: nrec - 1]) and not back[nrec - 1].any()

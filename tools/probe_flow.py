@@ -8,6 +8,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the phase probes exist only in the diagnostics build of the engine (make -C tools diag)
+os.environ.setdefault("CMPI_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcmpi_aead_tools.so"))
 import torch  # noqa: E402
 
 import bench  # noqa: E402

@@ -7,14 +7,14 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the phase probes exist only in the diagnostics build of the engine (make -C tools diag)
+os.environ.setdefault("CMPI_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcmpi_aead_tools.so"))
 import torch  # noqa: E402
 
 import bench  # noqa: E402
 from cryptmpi_2022_amd import _native as N  # noqa: E402
 
 res = {}
-if os.environ.get("SCHED"):
-    N.lib().cmpi_debug_set_sched(int(os.environ["SCHED"]))
 for wl in (sys.argv[1:] or ["gcm1k", "gcm4k"]):
     w = bench.Workload(wl, 0, seed=3)
     buf = torch.zeros(8 * 4096, dtype=torch.int64, device="cuda")

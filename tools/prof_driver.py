@@ -18,14 +18,6 @@ ap.add_argument("--seal-only", action="store_true")
 ap.add_argument("--out-stride", type=int, default=0,
                 help="gcm1k seal-only traffic calibration: output record stride (0 = dense n+16)")
 a = ap.parse_args()
-if os.environ.get("SCHED"):  # cmpi_debug_set_sched bits for the profiled run
-    from cryptmpi_2022_amd import _native as _N
-
-    _N.lib().cmpi_debug_set_sched(int(os.environ["SCHED"]))
-if os.environ.get("FORM"):  # cmpi_debug_set_gcm_form: 1 = the first lane-kernel form
-    from cryptmpi_2022_amd import _native as _N
-
-    _N.lib().cmpi_debug_set_gcm_form(int(os.environ["FORM"]))
 if a.out_stride:  # 65 536 x 1 KiB seals into records `out_stride` bytes apart (aligned vs dense)
     from cryptmpi_2022_amd import aead
 
