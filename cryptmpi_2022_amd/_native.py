@@ -102,6 +102,18 @@ _SIGS = {
     "cmpi_702_precompute": ([_P, _S, _I, _P], _I),
     "cmpi_702_recv_premask": ([_P, _P, _P, _P, _S, _P, _P], _I),
     "cmpi_702_recv": ([_P, _P, _P, _P, _S, _P, _P, _S, _P], _I),
+    "cmpi_602_seal_host_begin": ([_P, _P, _P, _P, _P, _U32, _U32, _P], _I),
+    "cmpi_602_seal_host": ([_P, _P, _P, _P, _P], _I),
+    "cmpi_602_open_host_begin": ([_P, _P, _P, _P, _U32, _U32, _P, _P], _I),
+    "cmpi_602_open_host": ([_P, _P, _P, _P, _P], _I),
+    "cmpi_700_send_host_begin": ([_P, _P, _P, _P, _S, _P, _P, _P], _I),
+    "cmpi_700_send_host": ([_P, _P, _P, _P, _S, _P, _P], _I),
+    "cmpi_700_recv_host_begin": ([_P, _P, _P, _P, _S, _P, _P], _I),
+    "cmpi_700_recv_host": ([_P, _P, _P, _P, _S, _P], _I),
+    "cmpi_702_send_host_begin": ([_P, _I, _P, _S, _P, _P, _P, _P], _I),
+    "cmpi_702_send_host": ([_P, _I, _P, _S, _P, _P], _I),
+    "cmpi_702_recv_host_begin": ([_P, _P, _P, _P, _S, _P, _P, _S, _P, _P], _I),
+    "cmpi_702_recv_host": ([_P, _P, _P, _P, _S, _P, _P, _S, _P], _I),
     "cmpi_gcm_seal_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P], _I),
     "cmpi_gcm_open_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
     "cmpi_ocb_seal_host_begin": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P], _I),

@@ -92,6 +92,10 @@ struct cmpi_req {
   uint8_t* h_out = nullptr;
   int32_t* h_status = nullptr;
   int32_t* user_status = nullptr;
+  size_t nst = 0;  // statuses to report (open): nrec for record batches, segments for framed messages
+  // framed requests (framed_host.hpp): pageable output spans copied from pinned staging at completion
+  std::vector<std::pair<uint8_t*, const uint8_t*>> span_dst;
+  std::vector<size_t> span_len;
   int error = CMPI_OK;
 };
 
@@ -181,6 +185,7 @@ int host_begin(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t
   r->device = c->device;
   r->dec = DEC;
   r->nrec = nrec;
+  r->nst = DEC ? nrec : 0;
   r->user_status = status;
   auto bail = [&](int rc) {
     if (r->st && r->done) (void)hipStreamSynchronize(r->st);
@@ -198,6 +203,7 @@ int host_begin(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t
   }
   if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess)
     return bail(fail(CMPI_EHIP, "event create failed"));
+  if ((rc = wait_keys(c, r->st))) return bail(rc);
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   if (nrec && nrec * (in_rec + out_rec) <= g_host_direct.load())
     return direct_begin<DEC, OCB>(c, P, r, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, req, bail);
@@ -272,11 +278,13 @@ int req_finish(cmpi_req* r) {
   DeviceGuard dg(r->device);
   int rc = r->error;
   if (!rc && r->unpack && r->nrec) par_copy_records(r->user_out, r->out_stride, r->h_out, r->op, r->out_rec, r->nrec);
-  if (!rc && r->dec && r->nrec) {
+  for (size_t i = 0; !rc && i < r->span_dst.size(); ++i)
+    par_copy_records(r->span_dst[i].first, r->span_len[i], r->span_dst[i].second, r->span_len[i], r->span_len[i], 1);
+  if (!rc && r->dec && r->nst) {
     size_t bad = 0;
-    for (size_t i = 0; i < r->nrec; ++i) bad += r->h_status[i] != 1;
-    if (r->user_status) memcpy(r->user_status, r->h_status, 4 * r->nrec);
-    if (bad) rc = fail(CMPI_EAUTH, "%zu of %zu records failed authentication", bad, r->nrec);
+    for (size_t i = 0; i < r->nst; ++i) bad += r->h_status[i] != 1;
+    if (r->user_status) memcpy(r->user_status, r->h_status, 4 * r->nst);
+    if (bad) rc = fail(CMPI_EAUTH, "%zu of %zu records failed authentication", bad, r->nst);
   }
   req_release(r);
   return rc;

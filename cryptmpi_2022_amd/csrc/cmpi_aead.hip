@@ -146,6 +146,10 @@ struct cmpi_ctx {
   mutable hipStream_t hstream = nullptr;
   mutable std::mutex hmu;                 // host-path pipeline (aead_host)
   std::unique_ptr<HostPipe> pipe{new HostPipe()};
+  // the last device re-key (cmpi_ctx_rekey / _rekey_subkey) on the caller's stream: the library's
+  // own streams (host paths, async requests) order their launches after it (wait_keys)
+  mutable hipEvent_t key_ev = nullptr;
+  mutable std::atomic<bool> key_pending{false};
 };
 
 namespace {
@@ -156,6 +160,27 @@ cmpi::dev::RoundKeys folded(const cmpi::dev::RoundKeys& k) {
   cmpi::dev::RoundKeys f = k;
   for (int i = 4; i < 40; ++i) f.w[i] = (k.w[i] << 16) | (k.w[i] >> 16);
   return f;
+}
+
+// Order a launch on one of the library's streams after the context's last device re-key.
+int wait_keys(const cmpi_ctx* c, hipStream_t st) {
+  if (!c->key_pending.load()) return CMPI_OK;
+  const hipError_t q = hipEventQuery(c->key_ev);
+  if (q == hipSuccess) {
+    c->key_pending.store(false);
+    return CMPI_OK;
+  }
+  if (q != hipErrorNotReady) return fail(CMPI_EHIP, "key setup failed: %s", hipGetErrorString(q));
+  HIP_TRY(hipStreamWaitEvent(st, c->key_ev, 0));
+  return CMPI_OK;
+}
+
+// After a re-key launched on `stream`: publish its completion event for wait_keys.
+int record_keys(const cmpi_ctx* c, hipStream_t stream) {
+  if (!c->key_ev) HIP_TRY(hipEventCreateWithFlags(&c->key_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(c->key_ev, stream));
+  c->key_pending.store(true);
+  return CMPI_OK;
 }
 
 int ensure_buf(void** p, size_t* cap, size_t need) {
@@ -849,6 +874,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
     P.init = true;
   }
+  if (int e = wait_keys(c, P.s[1])) return e;
   if (nrec * (in_rec + out_rec) <= g_host_direct.load())
     return host_direct<DEC, OCB>(c, P, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, status);
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -1178,6 +1204,10 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   if (c->hstream) (void)hipStreamSynchronize(c->hstream);
   if (c->scratch_used) (void)hipEventSynchronize(c->scratch_ev);
   if (c->scratch_ev) (void)hipEventDestroy(c->scratch_ev);
+  if (c->key_ev) {
+    (void)hipEventSynchronize(c->key_ev);
+    (void)hipEventDestroy(c->key_ev);
+  }
   if (c->scratch) (void)hipFree(c->scratch);
   for (auto& kv : c->chw) (void)hipFree(kv.second);
   if (c->stage) (void)hipFree(c->stage);
@@ -1477,7 +1507,7 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   hipLaunchKernelGGL(cmpi::dev::gcm_tables_kernel, dim3((cmpi::dev::kTabEntries + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, ta);
   HIP_TRY(hipGetLastError());
-  return CMPI_OK;
+  return record_keys(dst, (hipStream_t)stream);
 }
 
 // Re-key a context in place to a host-known key (no allocation, no host table build): the host
@@ -1536,8 +1566,11 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
     }
     HIP_TRY(hipMemcpyAsync(c->dt->ltab, lt, sizeof lt, hipMemcpyHostToDevice, (hipStream_t)stream));
   }
-  if (!stream) HIP_TRY(hipStreamSynchronize(nullptr));  // NULL stream: synchronous re-key
-  return CMPI_OK;
+  if (!stream) {
+    HIP_TRY(hipStreamSynchronize(nullptr));  // NULL stream: synchronous re-key
+    return CMPI_OK;
+  }
+  return record_keys(c, (hipStream_t)stream);
 }
 
 cmpi_ctx* cmpi_ctx_derive_subkey(const cmpi_ctx* base, const uint8_t v[16], void* stream) {
@@ -1576,3 +1609,4 @@ cmpi_ctx* cmpi_ctx_new_subkey(const cmpi_ctx* base, const uint8_t v[16]) {
 #include "ring_host.hpp"
 #include "ctrmode_host.hpp"
 #include "async_host.hpp"
+#include "framed_host.hpp"

@@ -63,11 +63,13 @@ std::vector<Seg602> segments_602(const cmpi_602_plan& p, uint32_t first, uint32_
 }
 
 // Run the segments as uniform batches.  nmode: seal 2 (prefix written), open 1 (prefix read).
-// small (n <= 65535, mode '1'): one segment keyed by the header nonce (nmode 3).
+// small (n <= 65535, mode '1'): one segment keyed by the header nonce (nmode 3).  The wire and
+// plaintext pointers address byte pt_base / w_base of the message (the host paths stage one outer
+// message's span at a time); status[k] is segment segs[0] + k.
 template <bool DEC>
 int run_602(const cmpi_ctx* c, const cmpi_602_plan& p, const uint8_t header[25], uint8_t* wire_out,
             const uint8_t* wire_in, uint8_t* pt_out, const uint8_t* pt_in, const std::vector<Seg602>& segs,
-            int32_t* status, void* stream) {
+            int32_t* status, void* stream, uint64_t pt_base = 0, uint64_t w_base = 0) {
   // small message (recv.c:401-440 / send.c:800-803): one segment under the header nonce
   const bool small = p.mode == '1' && p.total <= k602Pipe;
   size_t i = 0;
@@ -105,14 +107,14 @@ int run_602(const cmpi_ctx* c, const cmpi_602_plan& p, const uint8_t header[25],
       }
     }
     int rc;
+    const uint64_t po = s0.pt_off - pt_base, wo = s0.wire_off - w_base;
     if (!DEC) {
-      rc = gcm_batch<false>(c, wire_out + s0.wire_off + 5, w_stride, pt_in + s0.pt_off, pt_stride,
-                            small ? nullptr : wire_out + s0.wire_off, w_stride, s0.len, nrec, nullptr, nullptr,
-                            stream, ns);
+      rc = gcm_batch<false>(c, wire_out + wo + 5, w_stride, pt_in + po, pt_stride, small ? nullptr : wire_out + wo,
+                            w_stride, s0.len, nrec, nullptr, nullptr, stream, ns);
     } else {
-      rc = gcm_batch<true>(c, pt_out + s0.pt_off, pt_stride, wire_in + s0.wire_off + 5, w_stride,
-                           small ? nullptr : wire_in + s0.wire_off, w_stride, s0.len, nrec,
-                           status ? status + s0.ctr - segs[0].ctr : nullptr, nullptr, stream, ns);
+      rc = gcm_batch<true>(c, pt_out + po, pt_stride, wire_in + wo + 5, w_stride, small ? nullptr : wire_in + wo,
+                           w_stride, s0.len, nrec, status ? status + s0.ctr - segs[0].ctr : nullptr, nullptr,
+                           stream, ns);
     }
     if (rc) return rc;
     i = j;

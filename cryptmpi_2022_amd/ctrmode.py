@@ -82,3 +82,34 @@ def recv702(ctx, recv_iv: bytes, header: bytes, out, inp, mask=None, mask_len: i
     N.check(N.lib().cmpi_702_recv(ctx.handle, _b(recv_iv, 32), _b(header, HEADER), _dptr(out),
                                   out.numel() if out is not None else 0, _dptr(inp), _dptr(mask), mask_len,
                                   _stream_ptr(stream)))
+
+
+# ---- host-memory forms (numpy buffers; include/cmpi_ctrmode.h *_host)
+def _np(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def send700_host(ctx, send_iv: bytes, counter: int, out, inp, n: int):
+    """-> (header, next counter); out = ct (host, n bytes)."""
+    c = ctypes.c_uint64(counter)
+    hdr = (ctypes.c_uint8 * HEADER)()
+    N.check(N.lib().cmpi_700_send_host(ctx.handle, _b(send_iv, 16), ctypes.byref(c), _np(inp), n, hdr, _np(out)))
+    return bytes(hdr), c.value
+
+
+def recv700_host(ctx, recv_iv: bytes, header: bytes, out, inp) -> None:
+    N.check(N.lib().cmpi_700_recv_host(ctx.handle, _b(recv_iv, 16), _b(header, HEADER), _np(out), out.size, _np(inp)))
+
+
+def send702_host(sender: "Sender702", out, inp, n: int, pending_isends: int = 0) -> tuple[bytes, int]:
+    hdr = (ctypes.c_uint8 * HEADER)()
+    rc = N.lib().cmpi_702_send_host(sender._h, pending_isends, _np(inp), n, hdr, _np(out))
+    if rc < 0:
+        N.check(rc)
+    return bytes(hdr), rc
+
+
+def recv702_host(ctx, recv_iv: bytes, header: bytes, out, inp, mask=None, mask_len: int = 0, mask_stream=None) -> None:
+    """mask: device tensor from recv702_premask (made on mask_stream, default the current stream)."""
+    N.check(N.lib().cmpi_702_recv_host(ctx.handle, _b(recv_iv, 32), _b(header, HEADER), _np(out), out.size, _np(inp),
+                                       _dptr(mask), mask_len, _stream_ptr(mask_stream)))

@@ -74,3 +74,39 @@ def seal600(ctx, nonce: bytes, payload, inp, n: int, stream=None):
 
 def open600(ctx, out, payload, n: int, status=None, stream=None):
     N.check(N.lib().cmpi_600_open(ctx.handle, _dptr(out), _dptr(payload), n, _dptr(status), _stream_ptr(stream)))
+
+
+# ---- host-memory forms (numpy buffers; include/cmpi_frame.h *_host*): the 602 pipelined sender is
+# one seal602_host_begin per outer message, waited in order (send.c:729-850)
+def _np(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def seal602_host_begin(ctx, plan: Plan602, header: bytes, wire, inp, first: int, count: int = 1):
+    from .aead import Request
+
+    r = ctypes.c_void_p()
+    N.check(N.lib().cmpi_602_seal_host_begin(ctx.handle, ctypes.byref(plan), _hdr(header), _np(wire), _np(inp),
+                                             first, count, ctypes.byref(r)))
+    return Request(r, keep=(wire, inp))
+
+
+def seal602_host(ctx, plan: Plan602, header: bytes, wire, inp) -> None:
+    N.check(N.lib().cmpi_602_seal_host(ctx.handle, ctypes.byref(plan), _hdr(header), _np(wire), _np(inp)))
+
+
+def open602_host_begin(ctx, header: bytes, out, wire, first: int, count: int = 1, status=None):
+    from .aead import Request
+
+    r = ctypes.c_void_p()
+    N.check(N.lib().cmpi_602_open_host_begin(ctx.handle, _hdr(header), _np(out), _np(wire), first, count, _np(status),
+                                             ctypes.byref(r)))
+    return Request(r, keep=(out, wire, status))
+
+
+def open602_host(ctx, header: bytes, out, wire, status=None) -> int:
+    """-> CMPI_OK, or CMPI_EAUTH when a segment failed (status says which; zero-filled)."""
+    rc = N.lib().cmpi_602_open_host(ctx.handle, _hdr(header), _np(out), _np(wire), _np(status))
+    if rc not in (N.CMPI_OK, N.CMPI_EAUTH):
+        N.check(rc)
+    return rc

@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include "cmpi_aead.h"
+#include "cmpi_async.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -72,6 +73,31 @@ int cmpi_702_recv_premask(const cmpi_ctx *ctx, const uint8_t recv_iv[32], const 
  * refused (CMPI_EINVAL). */
 int cmpi_702_recv(const cmpi_ctx *ctx, const uint8_t recv_iv[32], const uint8_t header[26], uint8_t *out,
                   size_t out_cap, const uint8_t *in, const uint8_t *mask, size_t mask_len, void *stream);
+
+/* ---- host-memory forms (MPI user buffers, send.c:1716-1727 / :1768-1816):
+ * the same calls on host in/out buffers as requests on the library's pooled streams (cmpi_async.h),
+ * and their synchronous forms (begin + wait).  Headers, IVs and counters are updated when *_begin
+ * returns, exactly as by the device calls; page-locked buffers move by DMA, pageable ones through
+ * pinned staging.  702 receive: the mask stays device memory (cmpi_702_recv_premask on
+ * mask_stream while the payload is in flight); the request orders itself after mask_stream. */
+int cmpi_700_send_host_begin(const cmpi_ctx *ctx, const uint8_t send_iv[16], uint64_t *counter, const uint8_t *in,
+                             size_t n, uint8_t header[26], uint8_t *out, cmpi_req **req);
+int cmpi_700_send_host(const cmpi_ctx *ctx, const uint8_t send_iv[16], uint64_t *counter, const uint8_t *in, size_t n,
+                       uint8_t header[26], uint8_t *out);
+int cmpi_700_recv_host_begin(const cmpi_ctx *ctx, const uint8_t recv_iv[16], const uint8_t header[26], uint8_t *out,
+                             size_t out_cap, const uint8_t *in, cmpi_req **req);
+int cmpi_700_recv_host(const cmpi_ctx *ctx, const uint8_t recv_iv[16], const uint8_t header[26], uint8_t *out,
+                       size_t out_cap, const uint8_t *in);
+/* *segments = what cmpi_702_send returns (MPI_Isend segments); the sync form returns it. */
+int cmpi_702_send_host_begin(cmpi_702_sender *s, int pending_isends, const uint8_t *in, size_t n, uint8_t header[26],
+                             uint8_t *out, int *segments, cmpi_req **req);
+int cmpi_702_send_host(cmpi_702_sender *s, int pending_isends, const uint8_t *in, size_t n, uint8_t header[26],
+                       uint8_t *out);
+int cmpi_702_recv_host_begin(const cmpi_ctx *ctx, const uint8_t recv_iv[32], const uint8_t header[26], uint8_t *out,
+                             size_t out_cap, const uint8_t *in, const uint8_t *mask, size_t mask_len,
+                             void *mask_stream, cmpi_req **req);
+int cmpi_702_recv_host(const cmpi_ctx *ctx, const uint8_t recv_iv[32], const uint8_t header[26], uint8_t *out,
+                       size_t out_cap, const uint8_t *in, const uint8_t *mask, size_t mask_len, void *mask_stream);
 
 #ifdef __cplusplus
 }

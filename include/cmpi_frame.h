@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include "cmpi_aead.h"
+#include "cmpi_async.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -69,6 +70,30 @@ int cmpi_602_seal(const cmpi_ctx *seg_ctx, const cmpi_602_plan *plan, const uint
  * segments are zero-filled (aead.h:276-278). */
 int cmpi_602_open(const cmpi_ctx *seg_ctx, const uint8_t header[25], uint8_t *out, const uint8_t *wire,
                   int32_t *status, void *stream);
+
+/* ---- 602 from and to host memory (MPI user buffers) ----
+ * A request per call (cmpi_async.h: cmpi_test / cmpi_wait / cmpi_waitall), on the library's
+ * pooled streams: H2D of the call's host span, the device seal/open above, D2H of its result.
+ * Page-locked buffers move by DMA from / to the caller's pages; pageable ones through pinned
+ * staging (inputs packed inside *_begin, outputs copied out at completion).  The pipelined sender
+ * of send.c:729-850 is one seal_host_begin per outer message o (count 1) followed, in order, by
+ * cmpi_wait(req[o]) and MPI_Isend of cmpi_602_outer_span(o): outer o+1 is being sealed on the
+ * GPU while o is on the wire.  The receiver of recv.c:679-809 begins the open of each outer message
+ * as it lands.  A segment context re-keyed on a caller stream (cmpi_ctx_rekey_subkey) is ordered
+ * before these requests by the library.  Outputs must stay valid until the request completes. */
+int cmpi_602_seal_host_begin(const cmpi_ctx *seg_ctx, const cmpi_602_plan *plan, const uint8_t header[25],
+                             uint8_t *wire, const uint8_t *in, uint32_t first, uint32_t count, cmpi_req **req);
+/* every outer message begun, then all waited (the whole pipelined send) */
+int cmpi_602_seal_host(const cmpi_ctx *seg_ctx, const cmpi_602_plan *plan, const uint8_t header[25], uint8_t *wire,
+                       const uint8_t *in);
+/* open outer messages [first, first+count) of a received message: wire = the whole message's wire
+ * buffer (host), out = the whole plaintext (host, n bytes); status (host int32[plan nseg], may be
+ * NULL) gets the segments of those outers.  The wait returns CMPI_EAUTH when a segment failed (its
+ * plaintext zero-filled). */
+int cmpi_602_open_host_begin(const cmpi_ctx *seg_ctx, const uint8_t header[25], uint8_t *out, const uint8_t *wire,
+                             uint32_t first, uint32_t count, int32_t *status, cmpi_req **req);
+int cmpi_602_open_host(const cmpi_ctx *seg_ctx, const uint8_t header[25], uint8_t *out, const uint8_t *wire,
+                       int32_t *status);
 
 /* 600: header and payload of MPI_SEC_Multi_Thread_Send_OpenMP (kind '1') / isend (kind '2'). */
 int cmpi_600_header(uint32_t n, uint8_t kind, uint8_t header[25]);
