@@ -30,6 +30,7 @@ def _auto_plan():
     aead.force_wide(0, 0)
     aead.set_flow_threads(0)
     aead.set_flow_one_wg(True)
+    aead.set_flow_fuse(True)
     aead.N.lib().cmpi_debug_set_host_direct(DIRECT_DEFAULT)
 
 
@@ -220,13 +221,19 @@ def test_wide_decomposition(n, nrec, steps, one_wg):
 
 
 @pytest.mark.parametrize("threads", [1024, 512])
-@pytest.mark.parametrize("n,nrec,steps", [(64 * 16 * 3 - 16, 11, 1), (4097, 5, 2), (1 << 20, 2, 0)])
-def test_flow_kernel_forms(threads, n, nrec, steps):
-    """gcm_flow_kernel at 512 and 1024 threads per workgroup; 3-chunk records put up to six
-    records in one workgroup.  Two seals back to back, a forged record, and a context re-keyed
-    on the device (tables rebuilt by gcm_tables_kernel, bit-identical to the host build)."""
+@pytest.mark.parametrize("fuse", [True, False])
+@pytest.mark.parametrize("n,nrec,steps", [(64 * 16 * 3 - 16, 11, 1), (4097, 5, 2), (1 << 20, 2, 0),
+                                          ((1 << 20) - 5, 3, 1), (64 * 16 * 40 + 7, 37, 1)])
+def test_flow_kernel_forms(threads, fuse, n, nrec, steps):
+    """gcm_flow_kernel at 512 and 1024 threads per workgroup, finished by the last workgroup to
+    arrive (fuse) or by the XOR-combine launch; 3-chunk records put up to six records in one
+    workgroup, ragged lengths have a partial last block (write-through byte stores on the fused
+    open).  Two seals back to back (the arrival counters must return to zero), a forged record
+    (zero-filled by the last workgroup), and a context re-keyed on the device (tables rebuilt by
+    gcm_tables_kernel, bit-identical to the host build)."""
     aead.force_wide(1, steps)
     aead.set_flow_threads(threads)
+    aead.set_flow_fuse(fuse)
     key2 = bytes(range(100, 116))
     ctx = aead.AeadCtx(KEY)
     pt = records(0x5100 + n, nrec, n)
@@ -241,6 +248,38 @@ def test_flow_kernel_forms(threads, n, nrec, steps):
     assert not back[1].any() and np.array_equal(back[0], pt[0]) and np.array_equal(back[2:], pt[2:])
     ctx.rekey(key2)
     assert np.array_equal(gpu_seal(ctx, nonces, pt), oracle.gcm_seal_batch(key2, nonces, pt))
+    back, st = gpu_open(ctx, nonces, oracle.gcm_seal_batch(key2, nonces, pt))
+    assert list(st) == [1] * nrec and np.array_equal(back, pt)
+
+
+def test_flow_two_streams_one_fresh_context():
+    """calls on one context from two streams at once — the first use of a chunk-weight
+    table and of the fused completion's counters by either — stay correct: seals of 8 x 1 MiB and
+    3 x 100 000 B launched back to back on two streams of a fresh context, then opened the same way."""
+    import torch
+
+    ctx = aead.AeadCtx(KEY)
+    shapes = [(1 << 20, 8), (100000, 3)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    data = []
+    for (n, nrec), s in zip(shapes, streams):
+        pt = records(0x9100 + n, nrec, n)
+        nonces = random_nonces(0x9200 + n, nrec)
+        out = empty(nrec * (n + 16), fill=0)
+        data.append((n, nrec, pt, nonces, dev(pt), dev(nonces), out))
+    torch.cuda.synchronize()
+    for (n, nrec, _, _, d_pt, d_n, out), s in zip(data, streams):
+        ctx.seal_batch(out, d_pt, d_n, n, nrec, stream=s)
+    torch.cuda.synchronize()
+    outs = []
+    for (n, nrec, pt, nonces, _, d_n, out), s in zip(data, streams):
+        assert np.array_equal(host(out)[: nrec * (n + 16)].reshape(nrec, n + 16), oracle.gcm_seal_batch(KEY, nonces, pt))
+        back, st = empty(nrec * n, fill=0xAA), status_buf(nrec)
+        ctx.open_batch(back, out, d_n, n, nrec, status=st, stream=s)
+        outs.append((back, st))
+    torch.cuda.synchronize()
+    for (n, nrec, pt, *_), (back, st) in zip(data, outs):
+        assert (host(st)[:nrec] == 1).all() and np.array_equal(host(back)[: nrec * n].reshape(nrec, n), pt)
 
 
 @pytest.mark.parametrize("one_wg", [True, False])
