@@ -619,6 +619,7 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
     // the last workgroup: per-record XOR of every chunk partial into LDS accumulators (the tables
     // are no longer needed), 16 B per record at LDS 0
     for (uint32_t i = threadIdx.x; i < 4u * a.nrec; i += NT) lds_st32(4u * i, 0u);
+    if (threadIdx.x == 0u) lds_st32(kFlowFail + 4u, 0u);  // open: any record failed
     __syncthreads();
     for (uint32_t u0 = 0; u0 < units; u0 += NT) {
       const uint32_t u = u0 + threadIdx.x;
@@ -640,7 +641,6 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       }
     }
     __syncthreads();
-    uint32_t nfail = 0u;
     for (uint32_t r = threadIdx.x; r < a.nrec; r += NT) {
       const u32x4 y = lds128(16u * r);
       if (!DECRYPT) {
@@ -649,7 +649,7 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
         const u32x4 d = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len) ^ y;
         const bool ok = (d[0] | d[1] | d[2] | d[3]) == 0u;
         a.status[r] = ok ? 1 : 0;
-        nfail += ok ? 0u : 1u;
+        if (!ok) lds_st32(kFlowFail + 4u, 1u);
       }
     }
     if (threadIdx.x == 0u) {  // ready for the next launch: every workgroup has arrived
@@ -657,7 +657,9 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       for (uint32_t i = 0; i < 9u; ++i) __hip_atomic_store(a.fcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if constexpr (DECRYPT) {  // zero-fill forged records (aead.h:276-278), write-through like the plaintext
-      if (__syncthreads_or(nfail != 0u)) {
+      // (no __syncthreads_or: its static LDS word would sit at address 0, under record 0's accumulator)
+      __syncthreads();
+      if (lds32(kFlowFail + 4u)) {
         for (uint32_t r = 0; r < a.nrec; ++r) {
           const u32x4 d = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len) ^ lds128(16u * r);
           if ((d[0] | d[1] | d[2] | d[3]) == 0u) continue;  // workgroup-uniform
