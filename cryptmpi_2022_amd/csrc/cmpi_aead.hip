@@ -127,7 +127,6 @@ struct cmpi_ctx {
   cmpi::dev::RoundKeys rk{};
   cmpi::dev::RoundKeys drk{};
   Blk H{};
-  Blk fpow[10]{};           // H^1,2,3,4,8,12,16,32,48,64 (host-keyed GCM: gcm_flow_kernel's multipliers)
   DevTables* dt = nullptr;  // device
   // per-G combine multipliers H^{G·2^j}, j < 7 (host-keyed contexts; passed by value)
   mutable std::mutex mu;
@@ -527,12 +526,6 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.S = p.S;
     a.nch = p.nseg;
     a.wtab = reinterpret_cast<const u32x4*>(c->dt->fnib[0]);
-    if (c->dev_keys) {
-      a.fmulp = reinterpret_cast<const u32x4*>(c->dt->chains[0]);
-    } else {
-      static_assert(sizeof(Blk) == sizeof(u32x4), "field element layout");
-      memcpy(a.fmul, c->fpow, sizeof a.fmul);
-    }
     bool chw_transient = false;
     int rc = get_chw(c, p.G, p.nseg, &a.chw, st, &chw_transient);  // null for device-keyed contexts
     if (rc) return rc;
@@ -1190,10 +1183,8 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
     cmpi::build_byte_table(c->H, reinterpret_cast<Blk*>(ht->htab[0]));
     cmpi::build_byte_table(H2, reinterpret_cast<Blk*>(ht->htab[1]));
     cmpi::build_byte_table(H4, reinterpret_cast<Blk*>(ht->htab[2]));
-    for (uint32_t f = 0; f < cmpi::dev::kFlowNib; ++f) {
-      c->fpow[f] = cmpi::gf_pow(c->H, cmpi::dev::flow_nib_exp(f));
-      cmpi::build_nibble_table(c->fpow[f], reinterpret_cast<Blk*>(ht->fnib[f]));
-    }
+    for (uint32_t f = 0; f < cmpi::dev::kFlowNib; ++f)
+      cmpi::build_nibble_table(cmpi::gf_pow(c->H, cmpi::dev::flow_nib_exp(f)), reinterpret_cast<Blk*>(ht->fnib[f]));
   }
   if (alg == CMPI_AES_128_OCB) {
     // RFC 7253 §4.1: L_* = E_K(0), L_$ = double(L_*), L_0 = double(L_$), L_i = double(L_{i-1})
@@ -1582,7 +1573,6 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
   uint32_t z[4] = {0, 0, 0, 0}, h[4];
   cmpi::aes128_encrypt_words_host(c->rk.w, z, h);
   memcpy(c->H.b, h, 16);
-  for (uint32_t f = 0; f < cmpi::dev::kFlowNib; ++f) c->fpow[f] = cmpi::gf_pow(c->H, cmpi::dev::flow_nib_exp(f));
   c->dev_keys = false;
   hipLaunchKernelGGL(cmpi::dev::gcm_keysetup_kernel, dim3(1), dim3(256), cmpi::dev::kKsLds, (hipStream_t)stream, a);
   HIP_TRY(hipGetLastError());

@@ -66,11 +66,6 @@ struct GcmArgs {
   // the whole batch is one workgroup's units (every record's chunks together): the workgroup's
   // LDS aggregation finishes the tags, no second launch (host-keyed only)
   uint32_t one_wg;
-  // the FLOW kernel's ten multipliers H^1,2,3,4,8,12,16,32,48,64 (flow_nib_exp order): by value
-  // (host-keyed), or the key-setup kernel's basis chains in HBM (device-keyed: fmulp non-null,
-  // multiplier f = fmulp[128 * flow_nib_chain(f)]); the kernel builds its nibble tables from them
-  u32x4 fmul[10];
-  const u32x4* fmulp;
   // fused completion (gcm_flow_kernel<.., FUSE>): 9 arrival counters (8 workgroup groups + top),
   // zero between launches; the last workgroup to arrive XORs every record's partials
   uint32_t* fcnt;
@@ -354,23 +349,21 @@ __device__ __forceinline__ uint32_t flow_tab(uint32_t f) {  // nibble table f (k
   return f < 8u ? f * 8192u : 131072u + (f - 8u) * 8192u;
 }
 
-// Tables of the FLOW kernel: the AES row image from Te0 (1 KiB, L2-resident) and the ten nibble
-// tables BUILT in LDS from their ten multipliers (320 rows of 16 entries, one variable shift +
-// XORs each: nib_row_to_lds) — 160 B of multipliers instead of 80 KiB of tables fetched from L2
-// per workgroup.
+// Tables of the FLOW kernel: the AES row image from Te0 (1 KiB) and the ten nibble tables
+// (80 KiB), all loads issued before any LDS store (one L2 round trip).  (Measured, not taken:
+// building the nibble tables in LDS from their ten multipliers with nib_row_to_lds — 160 B fetched
+// instead of 80 KiB — staged at 5.4 us instead of 2.6 on 8 x 1 MiB: the 320 rows' VALU + 80 KiB
+// of ds_write_b128 cost more than the L2 round trip.)
 template <int NT>
 __device__ __forceinline__ void stage_flow(const GcmArgs& a) {
-  constexpr int kR = 1024 / NT;  // row-image loads per thread
+  constexpr int kR = 1024 / NT, kW = 5120 / NT;  // loads per thread
   uint32_t rv[kR];
+  u32x4 wv[kW];
   const uint32_t t = threadIdx.x;
 #pragma unroll
   for (int j = 0; j < kR; ++j) rv[j] = a.te0[(t + j * NT) >> 2];
-  if (t < kFlowNib) {  // the multipliers, parked in the aggregation slots until the tables are built
-    const u32x4 P = a.fmulp ? a.fmulp[128u * flow_nib_chain(t)] : a.fmul[t];
-    lds_st128(kFlowAgg + 16u * t, P);
-  }
-  __syncthreads();
-  for (uint32_t r = t; r < kFlowNib * 32u; r += NT) nib_row_to_lds(lds128(kFlowAgg + 16u * (r >> 5)), r & 31u, flow_tab(r >> 5));
+#pragma unroll
+  for (int j = 0; j < kW; ++j) wv[j] = a.wtab[t + j * NT];
 #pragma unroll
   for (int j = 0; j < kR; ++j) {  // row image: entry e -> 64 words (Te0 x32 | Te1 x32), 4 threads
     const uint32_t i = t + j * NT, e = i >> 2, q = i & 3u;
@@ -381,6 +374,11 @@ __device__ __forceinline__ void stage_flow(const GcmArgs& a) {
     lds_st128(o + 16u, w);
     lds_st128(o + 32u, w);
     lds_st128(o + 48u, w);
+  }
+#pragma unroll
+  for (int j = 0; j < kW; ++j) {
+    const uint32_t e = t + j * NT;
+    lds_st128(flow_tab(e >> 9) + (e & 511u) * 16u, wv[j]);
   }
   __syncthreads();
 }
@@ -621,10 +619,20 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
     for (uint32_t i = threadIdx.x; i < 4u * a.nrec; i += NT) lds_st32(4u * i, 0u);
     if (threadIdx.x == 0u) lds_st32(kFlowFail + 4u, 0u);  // open: any record failed
     __syncthreads();
-    for (uint32_t u0 = 0; u0 < units; u0 += NT) {
-      const uint32_t u = u0 + threadIdx.x;
-      u32x4 x = {0u, 0u, 0u, 0u};
-      if (u < units) x = fetch16(a.partial + u);
+    // every partial load of a pass in flight at once (a load per iteration paid the memory latency
+    // in sequence: 8.6 us for 2 048 partials)
+    constexpr uint32_t kPass = 8u;
+    for (uint32_t u0 = 0; u0 < units; u0 += kPass * NT) {
+      u32x4 xs[kPass];
+#pragma unroll
+      for (uint32_t j = 0; j < kPass; ++j) {
+        const uint32_t u = u0 + j * NT + threadIdx.x;
+        xs[j] = u < units ? fetch16(a.partial + u) : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kPass; ++j) {
+      const uint32_t u = u0 + j * NT + threadIdx.x;
+      u32x4 x = xs[j];
       const uint32_t r = u < units ? u / a.nch : 0xffffffffu;
       const uint32_t r0 = __builtin_amdgcn_readfirstlane(r);
       if (__builtin_amdgcn_ballot_w64(r != r0) == 0ull) {  // one record in the whole wave: reduce first
@@ -638,6 +646,7 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           __hip_atomic_fetch_xor((lds_u32*)(size_t)(16u * r + 4u * c), x[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       }
     }
     __syncthreads();
