@@ -276,12 +276,6 @@ def set_flow_one_wg(on: bool = True) -> None:
     N.lib().cmpi_debug_set_flow_one_wg(1 if on else 0)
 
 
-def set_flow_fuse(on: bool = True) -> None:
-    """Test hook (cmpi_debug_set_flow_fuse): multi-workgroup FLOW batches finish in the same launch
-    by the last workgroup to arrive (True, default) or through the XOR-combine launch (False)."""
-    N.lib().cmpi_debug_set_flow_fuse(1 if on else 0)
-
-
 def gcm_plan(ctx: AeadCtx, length: int, nrec: int):
     out = (ctypes.c_uint32 * 4)()
     N.check(N.lib().cmpi_debug_gcm_plan(ctx.handle, length, nrec, out))

@@ -140,9 +140,7 @@ struct cmpi_ctx {
   mutable size_t scratch_cap = 0;
   mutable hipEvent_t scratch_ev = nullptr;
   mutable bool scratch_used = false;
-  // arrival counters of the fused FLOW completion (9 words, zero between launches; ordered like
-  // the scratch: ScratchLease::order)
-  mutable uint32_t* fcnt = nullptr;
+
   mutable std::mutex smu;  // scratch lease (held through the launches of one call)
   mutable uint8_t* stage = nullptr;
   mutable size_t stage_cap = 0;
@@ -219,17 +217,6 @@ struct ScratchLease {
     if (c->scratch_used) HIP_TRY(hipStreamWaitEvent(st, c->scratch_ev, 0));
     return CMPI_OK;
   }
-  // the context's zeroed counters of the fused FLOW completion, allocated on first use
-  int counters(uint32_t** out) {
-    int rc = order();
-    if (rc) return rc;
-    if (!c->fcnt) {
-      HIP_TRY(hipMalloc(&c->fcnt, 64));
-      HIP_TRY(hipMemsetAsync(c->fcnt, 0, 64, st));
-    }
-    *out = c->fcnt;
-    return CMPI_OK;
-  }
   int acquire(size_t need) {
     if (ptr || !need) return CMPI_OK;
     int rc = order();
@@ -275,7 +262,6 @@ std::atomic<int> g_force_wide{0};       // wide decomposition: 0 automatic, 1 al
 std::atomic<uint32_t> g_force_S{0};     // wide steps per chunk, 0 = automatic
 std::atomic<int> g_flow_nt{0};          // FLOW kernel threads per workgroup: 0 automatic, 512 / 1024 forced
 std::atomic<int> g_flow_one_wg{1};      // FLOW kernel: one-workgroup batches finish their tags in-kernel
-std::atomic<int> g_flow_fuse{1};        // FLOW kernel: multi-workgroup batches finish by the last arriver
 #if CMPI_TOOLS
 std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics build: per-workgroup phase timestamps
 #endif
@@ -543,25 +529,19 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     // finished from the workgroup's LDS aggregation in the same launch
     const bool one_wg = a.chw && g_flow_one_wg.load() && waves <= (uint64_t)(NT / 64);
     a.one_wg = one_wg ? 1u : 0u;
-    // several workgroups, host-keyed: the last workgroup to arrive finishes the tags (no combine
-    // launch); its per-record accumulators take 16 B of LDS each
-    const bool fuse = a.chw && !one_wg && g_flow_fuse.load() && nrec <= 4096 && waves <= 65536;
-    if (fuse && (rc = lease.counters(&a.fcnt))) return rc;
-    if ((one_wg || fuse) && DEC && !status) a.status = reinterpret_cast<int32_t*>(ws + (size_t)nrec * p.nseg * 16);
+    if (one_wg && DEC && !status) a.status = reinterpret_cast<int32_t*>(ws + (size_t)nrec * p.nseg * 16);
     const bool dk = !a.chw;  // device-keyed context
     const void* fn = NT == 512 ? (dk ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, true>)
-                                  : fuse ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, false, true>)
-                                         : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, false>))
+                                     : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, false>))
                                : (dk ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, true>)
-                                  : fuse ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, false, true>)
-                                         : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, false>));
+                                     : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, false>));
     const size_t lds = (size_t)cmpi::dev::kFlowLds;
     if ((rc = set_lds_attr(fn, c->device, lds))) return rc;
     const uint32_t wpb = (uint32_t)NT / 64u;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + wpb - 1) / wpb, (uint64_t)c->ncu));
     void* kargs[] = {&a};
     HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(NT), kargs, lds, st));
-    if (one_wg || fuse) return CMPI_OK;
+    if (one_wg) return CMPI_OK;
     cmpi::dev::GcmCombineArgs ca{};
     ca.in = in;
     ca.out = out;
@@ -1230,7 +1210,6 @@ void cmpi_ctx_free(cmpi_ctx* c) {
     (void)hipEventDestroy(c->key_ev);
   }
   if (c->scratch) (void)hipFree(c->scratch);
-  if (c->fcnt) (void)hipFree(c->fcnt);
   for (auto& kv : c->chw) (void)hipFree(kv.second);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
@@ -1279,7 +1258,6 @@ void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
 void cmpi_debug_set_host_spin(int on) { g_host_spin.store(on ? 1 : 0); }
 
 void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }
-void cmpi_debug_set_flow_fuse(int on) { g_flow_fuse.store(on ? 1 : 0); }
 void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 || threads == 1024 ? threads : 0); }
 
 // Timing events without the system-scope release fence (hipEventDisableSystemFence): a default

@@ -66,9 +66,6 @@ struct GcmArgs {
   // the whole batch is one workgroup's units (every record's chunks together): the workgroup's
   // LDS aggregation finishes the tags, no second launch (host-keyed only)
   uint32_t one_wg;
-  // fused completion (gcm_flow_kernel<.., FUSE>): 9 arrival counters (8 workgroup groups + top),
-  // zero between launches; the last workgroup to arrive XORs every record's partials
-  uint32_t* fcnt;
 #if CMPI_TOOLS
   uint64_t* probe;  // per-WG phase timestamps (cmpi_debug_set_wide_probe), or null
 #endif
@@ -87,27 +84,6 @@ __device__ __forceinline__ RoundKeys load_round_keys(const RoundKeys& arg, const
 
 __device__ __forceinline__ u32x4 ld_blk(const uint8_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
 __device__ __forceinline__ void st_blk(uint8_t* p, u32x4 v) { *reinterpret_cast<u32x4a*>(p) = v; }
-// Write-through (sc1) stores: the bytes reach memory past this XCD's L2 and leave the line clean,
-// so a later store by another XCD (the fused FLOW completion's zero-fill of a forged record) is
-// never overwritten by a write-back of this one (MI355X_MICROARCH.md, Correctness boundaries).
-__device__ __forceinline__ void st_blk_wt(uint8_t* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_byte_wt(uint8_t* p, uint32_t v) {
-  asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-// 16 B published for other workgroups (two 8-B agent-scope stores, write-through) / read back
-__device__ __forceinline__ void publish16(u32x4* p, u32x4 v) {
-  uint64_t* q = reinterpret_cast<uint64_t*>(p);
-  __hip_atomic_store(q, (uint64_t)v[0] | ((uint64_t)v[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(q + 1, (uint64_t)v[2] | ((uint64_t)v[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u32x4 fetch16(const u32x4* p) {
-  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
-  const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-}
 // record data streamed once (MEM bit 0: loads, bit 1: stores) with the non-temporal policy
 template <int MEM>
 __device__ __forceinline__ u32x4 ld_rec(const uint8_t* p) {
@@ -427,13 +403,11 @@ __device__ __forceinline__ u32x4 flow_tree_r4(u32x4 acc, uint32_t lane) {
 // DK: device-keyed context (round keys loaded from HBM, partials weighted by the combine launch);
 // its own instantiation so the host-keyed form keeps its round keys as kernel arguments (the
 // runtime choice cost the host-keyed kernel 53 VGPRs and SGPR spills).
-// FUSE (host-keyed, several workgroups): no combine launch.  Every wave publishes its chunk
-// partial write-through; each workgroup, once its stores are performed, adds one to the counter of
-// its group (blockIdx % 8) and the group's last arriver to the top counter; the workgroup that
-// completes the top counter XORs every record's partials (agent-scope loads), writes the tags —
-// open: the verdicts, and zero-fills forged records — and resets the counters.  Open stores its
-// plaintext write-through so that zero-fill is final (no other XCD holds the lines dirty).
-template <bool DECRYPT, int NT, bool DK, bool FUSE = false>
+// (Measured, not taken: finishing multi-workgroup batches in the same launch — chunk partials
+// published write-through, per-group arrival counters, the last workgroup XORs every record's
+// partials and zero-fills forged records, plaintext stored write-through — 8 x 1 MiB seal 30.8 vs
+// 20.8 us, 1 x 64 KiB 19.4 vs 13.4 us with the XOR-combine launch: profiles/r03d_flow_fused_ab.txt.)
+template <bool DECRYPT, int NT, bool DK>
 __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
   CMPI_PROBE(a, 0u);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -505,17 +479,12 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
           uint8_t* op = out_rec + 16u * (uint32_t)p;
           if (full_blk(p)) {
             const u32x4 o = v ^ ks;
-            if (FUSE && DECRYPT) st_blk_wt(op, o);
-            else st_blk(op, o);
+            st_blk(op, o);
             x = DECRYPT ? v : o;
           } else {
             const u32x4 pp = load_partial(in_rec + 16u * (uint32_t)p, rem);
             const u32x4 o = mask_bytes(pp ^ ks, rem);
-            if (FUSE && DECRYPT) {
-              for (uint32_t b = 0; b < rem; ++b) st_byte_wt(op + b, o[b >> 2] >> (8u * (b & 3u)));
-            } else {
-              store_partial(op, o, rem);
-            }
+            store_partial(op, o, rem);
             x = DECRYPT ? pp : o;
           }
         } else if (p == nx - 1) {
@@ -556,10 +525,6 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       }
       if (first) CMPI_PROBE(a, 5u);
     }
-    if (FUSE) {  // partials for the last workgroup to arrive
-      if (u < units && lane == 0u) publish16(a.partial + u, pw);
-      continue;
-    }
     if (DK || !a.one_wg) {  // partials for the combine launch
       if (u < units && lane == 0u) a.partial[u] = pw;
       continue;
@@ -598,85 +563,6 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
         const uint32_t full4 = a.len & ~3u;
         for (uint32_t i = threadIdx.x * 4u; i < full4; i += NT * 4u) *reinterpret_cast<u32a*>(o + i) = 0u;
         for (uint32_t i = full4 + threadIdx.x; i < a.len; i += NT) o[i] = 0u;
-      }
-    }
-  }
-  if constexpr (FUSE) {
-    // arrival: this workgroup's partial (and plaintext) stores are performed, then one add
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0u) {
-      const uint32_t g = blockIdx.x & 7u, ng = gridDim.x < 8u ? gridDim.x : 8u, n_g = (gridDim.x - g + 7u) >> 3;
-      uint32_t last = 0u;
-      if (__hip_atomic_fetch_add(a.fcnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_g - 1u)
-        last = __hip_atomic_fetch_add(a.fcnt + 8u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1u ? 1u : 0u;
-      lds_st32(kFlowFail, last);
-    }
-    __syncthreads();
-    if (!lds32(kFlowFail)) return;
-    // the last workgroup: per-record XOR of every chunk partial into LDS accumulators (the tables
-    // are no longer needed), 16 B per record at LDS 0
-    for (uint32_t i = threadIdx.x; i < 4u * a.nrec; i += NT) lds_st32(4u * i, 0u);
-    if (threadIdx.x == 0u) lds_st32(kFlowFail + 4u, 0u);  // open: any record failed
-    __syncthreads();
-    // every partial load of a pass in flight at once (a load per iteration paid the memory latency
-    // in sequence: 8.6 us for 2 048 partials)
-    constexpr uint32_t kPass = 8u;
-    for (uint32_t u0 = 0; u0 < units; u0 += kPass * NT) {
-      u32x4 xs[kPass];
-#pragma unroll
-      for (uint32_t j = 0; j < kPass; ++j) {
-        const uint32_t u = u0 + j * NT + threadIdx.x;
-        xs[j] = u < units ? fetch16(a.partial + u) : u32x4{0u, 0u, 0u, 0u};
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < kPass; ++j) {
-      const uint32_t u = u0 + j * NT + threadIdx.x;
-      u32x4 x = xs[j];
-      const uint32_t r = u < units ? u / a.nch : 0xffffffffu;
-      const uint32_t r0 = __builtin_amdgcn_readfirstlane(r);
-      if (__builtin_amdgcn_ballot_w64(r != r0) == 0ull) {  // one record in the whole wave: reduce first
-#pragma unroll
-        for (int m = 1; m < 64; m <<= 1) x ^= shfl_xor4(x, m);
-        if (lane == 0u && r0 != 0xffffffffu)
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            __hip_atomic_fetch_xor((lds_u32*)(size_t)(16u * r0 + 4u * c), x[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else if (r != 0xffffffffu) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          __hip_atomic_fetch_xor((lds_u32*)(size_t)(16u * r + 4u * c), x[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      }
-    }
-    __syncthreads();
-    for (uint32_t r = threadIdx.x; r < a.nrec; r += NT) {
-      const u32x4 y = lds128(16u * r);
-      if (!DECRYPT) {
-        st_blk(a.out + (uint64_t)r * a.out_stride + a.len, y);
-      } else {
-        const u32x4 d = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len) ^ y;
-        const bool ok = (d[0] | d[1] | d[2] | d[3]) == 0u;
-        a.status[r] = ok ? 1 : 0;
-        if (!ok) lds_st32(kFlowFail + 4u, 1u);
-      }
-    }
-    if (threadIdx.x == 0u) {  // ready for the next launch: every workgroup has arrived
-#pragma unroll
-      for (uint32_t i = 0; i < 9u; ++i) __hip_atomic_store(a.fcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if constexpr (DECRYPT) {  // zero-fill forged records (aead.h:276-278), write-through like the plaintext
-      // (no __syncthreads_or: its static LDS word would sit at address 0, under record 0's accumulator)
-      __syncthreads();
-      if (lds32(kFlowFail + 4u)) {
-        for (uint32_t r = 0; r < a.nrec; ++r) {
-          const u32x4 d = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len) ^ lds128(16u * r);
-          if ((d[0] | d[1] | d[2] | d[3]) == 0u) continue;  // workgroup-uniform
-          uint8_t* o = a.out + (uint64_t)r * a.out_stride;
-          const uint32_t full16 = a.len & ~15u;
-          for (uint32_t i = threadIdx.x * 16u; i < full16; i += NT * 16u) st_blk_wt(o + i, u32x4{0u, 0u, 0u, 0u});
-          for (uint32_t i = full16 + threadIdx.x; i < a.len; i += NT) st_byte_wt(o + i, 0u);
-        }
       }
     }
   }

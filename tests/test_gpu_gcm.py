@@ -30,7 +30,6 @@ def _auto_plan():
     aead.force_wide(0, 0)
     aead.set_flow_threads(0)
     aead.set_flow_one_wg(True)
-    aead.set_flow_fuse(True)
     aead.N.lib().cmpi_debug_set_host_direct(DIRECT_DEFAULT)
 
 
@@ -221,19 +220,15 @@ def test_wide_decomposition(n, nrec, steps, one_wg):
 
 
 @pytest.mark.parametrize("threads", [1024, 512])
-@pytest.mark.parametrize("fuse", [True, False])
 @pytest.mark.parametrize("n,nrec,steps", [(64 * 16 * 3 - 16, 11, 1), (4097, 5, 2), (1 << 20, 2, 0),
                                           ((1 << 20) - 5, 3, 1), (64 * 16 * 40 + 7, 37, 1)])
-def test_flow_kernel_forms(threads, fuse, n, nrec, steps):
-    """gcm_flow_kernel at 512 and 1024 threads per workgroup, finished by the last workgroup to
-    arrive (fuse) or by the XOR-combine launch; 3-chunk records put up to six records in one
-    workgroup, ragged lengths have a partial last block (write-through byte stores on the fused
-    open).  Two seals back to back (the arrival counters must return to zero), a forged record
-    (zero-filled by the last workgroup), and a context re-keyed on the device (tables rebuilt by
-    gcm_tables_kernel, bit-identical to the host build)."""
+def test_flow_kernel_forms(threads, n, nrec, steps):
+    """gcm_flow_kernel at 512 and 1024 threads per workgroup; 3-chunk records put up to six
+    records in one workgroup, ragged lengths have a partial last block.  Two seals back to back,
+    a forged record, and a context re-keyed on the device (tables rebuilt by gcm_tables_kernel,
+    bit-identical to the host build)."""
     aead.force_wide(1, steps)
     aead.set_flow_threads(threads)
-    aead.set_flow_fuse(fuse)
     key2 = bytes(range(100, 116))
     ctx = aead.AeadCtx(KEY)
     pt = records(0x5100 + n, nrec, n)
