@@ -17,6 +17,7 @@
 //    libcrypto's EVP_aes_256_ecb() at init.c:848 when SYMMETRIC_KEY_SIZE is 32) is forwarded to
 //    the next libcrypto in the link order (dlsym RTLD_NEXT) on a real EVP_CIPHER_CTX the shim
 //    keeps inside its own; without one the call fails (returns 0) instead of misreading it.
+#include <sys/random.h>
 #include <dlfcn.h>
 #include <stdlib.h>
 #include <string.h>
@@ -92,10 +93,14 @@ int pick_device() {
   return 0;
 }
 
+// Live contexts are shared by key (CryptMPI's OpenMP team seals on one global context); a freed
+// context keeps no key material: its key is wiped and the engine context re-keyed to a random key
+// (device schedule and tables overwritten) before it joins the idle list, from which the next
+// EVP_AEAD_CTX_new re-keys it (BoringSSL wipes key material on free).
 struct Pool {
   std::mutex m;
-  std::map<Key, Shared*> by_key;  // live and idle contexts
-  std::list<Shared*> idle;        // refs == 0, oldest first
+  std::map<Key, Shared*> by_key;  // live contexts (refs > 0)
+  std::list<Shared*> idle;        // refs == 0, scrubbed, oldest first
 };
 Pool& pool() {
   static Pool* p = new Pool();  // never destroyed: contexts may be freed from atexit handlers
@@ -103,13 +108,28 @@ Pool& pool() {
 }
 
 void destroy(Shared* s) {
-  cmpi_ctx_free(s->c);
+  cmpi_ctx_free(s->c);  // wipes the engine's host copy of the key
   if (s->stage) {
     (void)cmpi_host_unregister(s->stage);
     free(s->stage);
   }
-  s->key.fill(0);
+  explicit_bzero(s->key.data(), s->key.size());
   delete s;
+}
+
+// Idle context: no key material left behind (host key wiped, device schedule re-keyed at random).
+bool scrub(Shared* s) {
+  explicit_bzero(s->key.data(), s->key.size());
+  uint8_t rnd[16];
+  size_t got = 0;
+  while (got < sizeof rnd) {
+    const ssize_t r = getrandom(rnd + got, sizeof rnd - got, 0);
+    if (r <= 0) return false;
+    got += (size_t)r;
+  }
+  const bool ok = cmpi_ctx_rekey(s->c, rnd, 16, nullptr) == CMPI_OK;
+  explicit_bzero(rnd, sizeof rnd);
+  return ok;
 }
 
 Shared* acquire(const uint8_t* key) {
@@ -118,16 +138,16 @@ Shared* acquire(const uint8_t* key) {
   Pool& P = pool();
   std::lock_guard<std::mutex> lk(P.m);
   auto it = P.by_key.find(k);
-  if (it != P.by_key.end()) {  // same key: share (or revive from the idle list)
+  if (it != P.by_key.end()) {  // same key as a live context: share it
     Shared* s = it->second;
-    if (s->refs++ == 0) P.idle.remove(s);
+    ++s->refs;
+    explicit_bzero(k.data(), k.size());
     return s;
   }
   Shared* s = nullptr;
   if (!P.idle.empty()) {  // re-key the oldest idle context on the device
     s = P.idle.front();
     P.idle.pop_front();
-    P.by_key.erase(s->key);
     if (cmpi_ctx_rekey(s->c, key, 16, nullptr) != CMPI_OK) {
       destroy(s);
       s = nullptr;
@@ -142,6 +162,7 @@ Shared* acquire(const uint8_t* key) {
   s->key = k;
   s->refs = 1;
   P.by_key[k] = s;
+  explicit_bzero(k.data(), k.size());
   return s;
 }
 
@@ -149,8 +170,8 @@ void release(Shared* s) {
   Pool& P = pool();
   std::lock_guard<std::mutex> lk(P.m);
   if (--s->refs > 0) return;
-  if (kIdleCap == 0) {
-    P.by_key.erase(s->key);
+  P.by_key.erase(s->key);
+  if (kIdleCap == 0 || !scrub(s)) {
     destroy(s);
     return;
   }
@@ -158,7 +179,6 @@ void release(Shared* s) {
   while (P.idle.size() > kIdleCap) {
     Shared* o = P.idle.front();
     P.idle.pop_front();
-    P.by_key.erase(o->key);
     destroy(o);
   }
 }
