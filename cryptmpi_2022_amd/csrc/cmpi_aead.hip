@@ -640,20 +640,6 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   u32x4* d_off0 = reinterpret_cast<u32x4*>(ws + part_bytes);
   int32_t* st_arr = status ? status : reinterpret_cast<int32_t*>(ws + part_bytes + off_bytes);
 
-  cmpi::dev::OcbOffsetArgs oa{};
-  oa.nonces = nonces;
-  oa.nonce_stride = nonce_stride;
-  oa.nrec = (uint32_t)nrec;
-  oa.te0 = c->dt->te0;
-  oa.off0 = d_off0;
-  oa.rk = folded(c->rk);
-  {
-    int rc0 = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ocb_offset_kernel), c->device, 65536);
-    if (rc0) return rc0;
-  }
-  hipLaunchKernelGGL(cmpi::dev::ocb_offset_kernel, dim3((uint32_t)((nrec + 255) / 256)), dim3(256), 65536, st, oa);
-  HIP_TRY(hipGetLastError());
-
   cmpi::dev::OcbArgs a{};
   a.in = in;
   a.out = out;
@@ -676,7 +662,7 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   a.rk = folded(c->rk);
   a.sched = kSched;
   a.drk = folded(c->drk);
-  const size_t lds = DEC ? cmpi::dev::kOcbLdsOpen : cmpi::dev::kOcbLdsSeal;
+  const size_t lds = DEC ? cmpi::dev::kOcbBatchLdsOpen : cmpi::dev::kOcbBatchLdsSeal;
   const uint32_t per_cu = DEC ? 1u : 2u;  // LDS-limited 1024-thread blocks per CU
   auto fn = cmpi::dev::ocb_batch_kernel<DEC>;
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds);
@@ -704,17 +690,12 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   f.status = st_arr;
   f.rk = folded(c->rk);
   {
-    int rc1 = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ocb_final_kernel<DEC>), c->device, cmpi::dev::kOcbLdsSeal);
+    int rc1 = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ocb_final_kernel<DEC>), c->device, cmpi::dev::kOcbFinalLds);
     if (rc1) return rc1;
   }
   hipLaunchKernelGGL(cmpi::dev::ocb_final_kernel<DEC>, dim3((uint32_t)((nrec + 255) / 256)), dim3(256),
-                     cmpi::dev::kOcbLdsSeal, st, f);
+                     cmpi::dev::kOcbFinalLds, st, f);  // open: verdicts and the zero-fill of forged records
   HIP_TRY(hipGetLastError());
-  if (DEC) {
-    hipLaunchKernelGGL(cmpi::dev::zero_failed_kernel, dim3((uint32_t)nrec), dim3(256), 0, st, out,
-                       (uint64_t)out_stride, (uint32_t)len, (const int32_t*)st_arr);
-    HIP_TRY(hipGetLastError());
-  }
   return CMPI_OK;
 }
 
