@@ -462,21 +462,15 @@ __device__ __forceinline__ void rotate_prio(uint32_t t) {
 // counter holds the sum of all waves' progress).  Waves of equal work then finish together
 // instead of spread by issue arbitration (tools/probe/lds_probe.hip, 4 waves/SIMD: 2.71 -> 2.48
 // CU-ns per block against rotate_prio, wave lifetimes 288K..375K -> 347K..362K cycles).
-// backoff > 0: a wave more than `backoff` slots ahead of the workgroup average sleeps (re-reading
-// the counter, at most 32 times per slot) so that the waves of slower SIMDs get the CU's LDS
-// bandwidth: priority alone only arbitrates among the waves of one SIMD.
-__device__ __forceinline__ void progress_prio(uint32_t cnt_off, uint32_t done, uint32_t backoff = 0u) {
+// Measured, not taken: a bounded s_sleep back-off of waves more than 4/8/16 slots ahead of the
+// average (to hand the CU's LDS to slower SIMDs) left config 2 at 57.5-57.9 us per seal (warm
+// clocks, tools/lane_ab.py, profiles/r03e_lane_backoff_ab.log).
+__device__ __forceinline__ void progress_prio(uint32_t cnt_off, uint32_t done) {
   uint32_t tot = 0;
   if ((threadIdx.x & 63u) == 0u)
     tot = __hip_atomic_fetch_add((lds_u32*)(size_t)cnt_off, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   tot = __builtin_amdgcn_readfirstlane(tot) + 1u;
   const uint32_t nw = blockDim.x >> 6, mine = done * nw;
-  if (backoff) {
-    for (uint32_t i = 0; i < 32u && mine > tot + backoff * nw; ++i) {
-      __builtin_amdgcn_s_sleep(2);
-      tot = __builtin_amdgcn_readfirstlane(lds32(cnt_off));
-    }
-  }
   const uint32_t p = mine + nw <= tot ? 3u : (mine <= tot ? 2u : (mine <= tot + nw ? 1u : 0u));
   switch (p) {
     case 0: __builtin_amdgcn_s_setprio(0); break;

@@ -262,7 +262,6 @@ std::atomic<int> g_force_wide{0};       // wide decomposition: 0 automatic, 1 al
 std::atomic<uint32_t> g_force_S{0};     // wide steps per chunk, 0 = automatic
 std::atomic<int> g_flow_nt{0};          // FLOW kernel threads per workgroup: 0 automatic, 512 / 1024 forced
 std::atomic<int> g_flow_one_wg{1};      // FLOW kernel: one-workgroup batches finish their tags in-kernel
-std::atomic<uint32_t> g_lane_backoff{0}; // lane kernel: progress back-off margin (slots), 0 = off
 #if CMPI_TOOLS
 std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics build: per-workgroup phase timestamps
 #endif
@@ -566,7 +565,6 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.ekj0 = reinterpret_cast<u32x4*>(ws + (size_t)nrec * p.nseg * 16);
   }
   const size_t lds = cmpi::dev::gcm_lds_bytes(p.L);
-  a.backoff = g_lane_backoff.load();
   const uint64_t want = ((uint64_t)a.ngroups * p.L + kGcmThreads - 1) / kGcmThreads;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->ncu));
   int rc;
@@ -1241,7 +1239,6 @@ void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
 void cmpi_debug_set_host_spin(int on) { g_host_spin.store(on ? 1 : 0); }
 
 void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }
-void cmpi_debug_set_lane_backoff(uint32_t slots) { g_lane_backoff.store(slots); }
 void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 || threads == 1024 ? threads : 0); }
 
 // Timing events without the system-scope release fence (hipEventDisableSystemFence): a default

@@ -66,7 +66,6 @@ struct GcmArgs {
   // the whole batch is one workgroup's units (every record's chunks together): the workgroup's
   // LDS aggregation finishes the tags, no second launch (host-keyed only)
   uint32_t one_wg;
-  uint32_t backoff;  // lane kernel: progress_prio back-off margin in slots (0 = off)
 #if CMPI_TOOLS
   uint64_t* probe;  // per-WG phase timestamps (cmpi_debug_set_wide_probe), or null
 #endif
@@ -226,7 +225,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
       auto ld = [&](uint32_t uu) { return ld_blk(ip + 16u * (uu < nfull ? uu : nfull - 1u)); };
       u32x4 v = ld(q);
       for (uint32_t u = q; u < nfull; u += (uint32_t)L) {
-        progress_prio(gcm_prog_off(L), ++done, a.backoff);
+        progress_prio(gcm_prog_off(L), ++done);
         const u32x4 o = v ^ keystream(2u + x0 + u);
         st_blk(op + 16u * u, o);
         acc = gmul_byte(acc, gl, DECRYPT ? v : o);

@@ -38,9 +38,6 @@ void cmpi_debug_set_flow_threads(int threads);
 /* FLOW kernel: a batch whose chunks all fit one workgroup finishes its tags in-kernel (1, default)
  * or through the XOR-combine launch (0). */
 void cmpi_debug_set_flow_one_wg(int on);
-/* GCM lane kernel: a wave more than `slots` slots ahead of its workgroup's average progress
- * sleeps briefly (bounded) to leave the CU's LDS to the waves of slower SIMDs; 0 = off. */
-void cmpi_debug_set_lane_backoff(uint32_t slots);
 /* Host-memory calls (cmpi_*_host) up to `bytes` of input + output records run the direct path
  * (kernel on page-locked host memory, no DMA); larger ones the 3-stream pipeline.  0 = never. */
 void cmpi_debug_set_host_direct(size_t bytes);

@@ -6,6 +6,7 @@ usage: tools/lane_ab.py <hook> <value,value,...> [workloads]"""
 import json
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
@@ -20,7 +21,7 @@ def main():
     wls = sys.argv[3].split(",") if len(sys.argv) > 3 else ["gcm1k", "gcm4k"]
     L = N.lib()
     set_ = getattr(L, hook)
-    iters, rounds = 30, 5
+    iters, rounds = 30, 7
     res = {}
     for wl in wls:
         w = bench.Workload(wl, 0, seed=11)
@@ -31,10 +32,12 @@ def main():
         for r in range(rounds):
             for v in vals:
                 set_(v)
-                for _ in range(10):
-                    w.seal()
-                    w.open()
-                torch.cuda.synchronize()
+                t_w = time.perf_counter()  # >= 0.3 s of warm-up per arm: clocks at steady state
+                while time.perf_counter() - t_w < 0.3:
+                    for _ in range(8):
+                        w.seal()
+                        w.open()
+                    torch.cuda.synchronize()
                 ev.record(0, st)
                 for i in range(iters):
                     w.seal()
