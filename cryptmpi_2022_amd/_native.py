@@ -56,6 +56,9 @@ _SIGS = {
     "cmpi_ctx_device": ([_P], _I),
     "cmpi_host_register": ([_P, _S], _I),
     "cmpi_host_unregister": ([_P], _I),
+    "cmpi_service_start": ([_P, _U32], _I),
+    "cmpi_service_stop": ([_P], _I),
+    "cmpi_service_running": ([_P], _I),
     "cmpi_gcm_workspace_size": ([_P, _S, _S], _S),
     "cmpi_gcm_seal_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P], _I),
     "cmpi_gcm_open_batch": ([_P, _P, _S, _P, _S, _P, _S, _S, _S, _P, _P, _P], _I),

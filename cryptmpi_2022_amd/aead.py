@@ -108,6 +108,19 @@ class AeadCtx(_Ctx):
         vb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(v))
         N.check(N.lib().cmpi_ctx_rekey_subkey(self._h, base.handle, vb, _stream_ptr(stream)))
 
+    # ------------------------------------------------------------ resident message service
+    def service_start(self, idle_us: int = 0) -> None:
+        """Serve this context's single host messages (seal_host/open_host with nrec = 1,
+        <= 512 KiB) from a resident kernel (include/cmpi_service.h); it returns its CUs after
+        `idle_us` (0 = 2000) without a message and restarts on the next."""
+        N.check(N.lib().cmpi_service_start(self._h, idle_us))
+
+    def service_stop(self) -> None:
+        N.check(N.lib().cmpi_service_stop(self._h))
+
+    def service_running(self) -> bool:
+        return bool(N.lib().cmpi_service_running(self._h))
+
     # ------------------------------------------------------------ device-resident batches
     def seal_batch(self, out, inp, nonces, length: int, nrec: int, *, in_stride=None, out_stride=None,
                    nonce_stride=NONCE_LEN, workspace=None, stream=None) -> None:

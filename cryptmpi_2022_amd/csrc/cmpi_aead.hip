@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -113,8 +114,15 @@ struct HostPipe {
   size_t hst_cap = 0;
   uint8_t* dbounce = nullptr;  // pinned: direct path's packed pageable records, nonces, statuses
   size_t dcap = 0;
+  uint32_t* hflag = nullptr;  // pinned coherent word: the direct path's completion sequence number
+  uint32_t* dflag = nullptr;  // its device address
+  uint32_t seq = 0;
   bool init = false;
 };
+
+namespace {
+struct Svc;  // resident message service (service_host.hpp)
+}
 
 struct cmpi_ctx {
   int alg = 0;
@@ -151,6 +159,7 @@ struct cmpi_ctx {
   // own streams (host paths, async requests) order their launches after it (wait_keys)
   mutable hipEvent_t key_ev = nullptr;
   mutable std::atomic<bool> key_pending{false};
+  Svc* svc = nullptr;  // cmpi_service_start (guarded by hmu)
 };
 
 namespace {
@@ -762,14 +771,55 @@ void* pinned_dev_ptr(const void* p) {
   return (uint8_t*)at.devicePointer + off;
 }
 
-// Wait for a stream by polling it (an MPI progress loop's busy wait): the blocking
-// hipStreamSynchronize sleeps and adds its wake-up latency to every small message.
-std::atomic<int> g_host_spin{1};
-hipError_t spin_sync(hipStream_t st) {
-  if (!g_host_spin.load()) return hipStreamSynchronize(st);
-  for (;;) {
-    const hipError_t e = hipStreamQuery(st);
-    if (e != hipErrorNotReady) return e;
+// Completion of a direct-path call (an MPI progress loop's busy wait).  g_host_spin selects how
+// the host learns that the call's kernels are done:
+//   0  blocking hipStreamSynchronize;
+//   1  the stream writes the call's sequence number into a page-locked coherent host word after
+//      the kernels (hipStreamWriteValue32) and the host spins on that word;
+//   2  the same word written by a one-wave kernel launched after the call's kernels;
+//   3  polling hipStreamQuery (the round-2 form).
+// In modes 1 and 2 the loop also asks the stream after 200 us, so a failed kernel returns its
+// error instead of spinning.
+std::atomic<int> g_host_spin{0};
+__global__ void done_flag_kernel(uint32_t* flag, uint32_t seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+hipError_t flag_wait(HostPipe& P, hipStream_t st) {
+  const int mode = g_host_spin.load();
+  if (mode == 0) return hipStreamSynchronize(st);
+  if (mode == 3) {
+    for (;;) {
+      const hipError_t e = hipStreamQuery(st);
+      if (e != hipErrorNotReady) return e;
+    }
+  }
+  if (!P.hflag) {
+    hipError_t e = hipHostMalloc((void**)&P.hflag, 64, hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    *P.hflag = P.seq;
+    if ((e = hipHostGetDevicePointer((void**)&P.dflag, P.hflag, 0)) != hipSuccess) {
+      (void)hipHostFree(P.hflag);
+      P.hflag = nullptr;
+      return e;
+    }
+  }
+  const uint32_t seq = ++P.seq;
+  hipError_t e = hipSuccess;
+  if (mode == 1) {
+    e = hipStreamWriteValue32(st, P.dflag, seq, 0);
+  } else {
+    done_flag_kernel<<<1, 64, 0, st>>>(P.dflag, seq);
+    e = hipGetLastError();
+  }
+  if (e != hipSuccess) return e;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1;; ++i) {
+    if (__atomic_load_n(P.hflag, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+    if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+      e = hipStreamQuery(st);
+      if (e == hipSuccess) return __atomic_load_n(P.hflag, __ATOMIC_ACQUIRE) == seq ? hipSuccess : hipErrorUnknown;
+      if (e != hipErrorNotReady) return e;
+    }
   }
 }
 
@@ -823,7 +873,7 @@ int host_direct(const cmpi_ctx* c, HostPipe& P, uint8_t* out, size_t out_stride,
                : gcm_batch<DEC>(c, (uint8_t*)dout, ostr, (const uint8_t*)din, istr, dB + bi + bo, 16, len, nrec,
                                DEC ? dst : nullptr, nullptr, P.s[1]);
   if (rc) return rc;
-  HIP_TRY(spin_sync(P.s[1]));
+  HIP_TRY(flag_wait(P, P.s[1]));
   if (hout && out_rec) par_copy_records(out, out_stride, hout, out_rec, out_rec, nrec);
   if (DEC) {
     size_t bad = 0;
@@ -833,6 +883,10 @@ int host_direct(const cmpi_ctx* c, HostPipe& P, uint8_t* out, size_t out_stride,
   }
   return CMPI_OK;
 }
+
+}  // namespace
+#include "service_host.hpp"
+namespace {
 
 template <bool DEC, bool OCB>
 int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
@@ -857,6 +911,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     P.init = true;
   }
   if (int e = wait_keys(c, P.s[1])) return e;
+  if (!OCB && c->svc && nrec == 1 && len <= kSvcMaxLen)  // the resident service (opt-in)
+    return svc_call<DEC>(c, *c->svc, out, in, nonces, len, status);
   if (nrec * (in_rec + out_rec) <= g_host_direct.load())
     return host_direct<DEC, OCB>(c, P, out, out_stride, in, in_stride, nonces, nonce_stride, len, nrec, status);
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -1177,6 +1233,10 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
 void cmpi_ctx_free(cmpi_ctx* c) {
   if (!c) return;
   DeviceGuard dg(c->device);
+  {
+    std::lock_guard<std::mutex> hl(c->hmu);
+    (void)svc_shutdown_locked(c);
+  }
   // Drain the context's own streams and its scratch's last user (not the whole device: the
   // per-message 602 path frees contexts at message rate).  Device-resident calls the caller
   // enqueued on its own streams must be complete or ordered before the free, as for any buffer
@@ -1208,6 +1268,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
     if (P.hbuf) (void)hipHostFree(P.hbuf);
     if (P.hst) (void)hipHostFree(P.hst);
     if (P.dbounce) (void)hipHostFree(P.dbounce);
+    if (P.hflag) (void)hipHostFree(P.hflag);
   }
   if (c->dt) (void)hipFree(c->dt);
   memset(c->key, 0, 16);
@@ -1236,7 +1297,7 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
 }
 
 void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
-void cmpi_debug_set_host_spin(int on) { g_host_spin.store(on ? 1 : 0); }
+void cmpi_debug_set_host_spin(int mode) { g_host_spin.store(mode >= 0 && mode <= 3 ? mode : 0); }
 
 void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }
 void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 || threads == 1024 ? threads : 0); }
@@ -1468,6 +1529,7 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
     // tables: drain them first.  Work the caller enqueued on other streams of its own must be
     // ordered before `stream` by the caller (cmpi_aead.h: derived contexts are stream-ordered).
     std::lock_guard<std::mutex> hl(dst->hmu);
+    if (int e = svc_shutdown_locked(dst)) return e;  // a device-keyed context has no service
     if (dst->pipe && dst->pipe->init)
       for (auto& ps : dst->pipe->s) HIP_TRY(hipStreamSynchronize(ps));
     if (dst->hstream) HIP_TRY(hipStreamSynchronize(dst->hstream));
@@ -1517,6 +1579,10 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
   if (rc) return rc;
   {
     std::lock_guard<std::mutex> hl(c->hmu);
+    if (c->svc) {  // the service holds the old key and tables: the next message relaunches it
+      if (int e = svc_stop_locked(*c->svc)) return e;
+      c->svc->wts_ok = false;
+    }
     if (c->pipe && c->pipe->init)
       for (auto& ps : c->pipe->s) HIP_TRY(hipStreamSynchronize(ps));
     if (c->hstream) HIP_TRY(hipStreamSynchronize(c->hstream));

@@ -407,28 +407,125 @@ __device__ __forceinline__ u32x4 flow_tree_r4(u32x4 acc, uint32_t lane) {
 // published write-through, per-group arrival counters, the last workgroup XORs every record's
 // partials and zero-fills forged records, plaintext stored write-through — 8 x 1 MiB seal 30.8 vs
 // 20.8 us, 1 x 64 KiB 19.4 vs 13.4 us with the XOR-combine launch: profiles/r03d_flow_fused_ab.txt.)
+// Unit u = (record r, chunk i) of a flow decomposition: chunk 0 absorbs the remainder (r0 X-blocks,
+// ceil(r0/64) steps), the others are C = 64·S X-blocks; returns the base X position of lane 0's
+// first step.
+__device__ __forceinline__ int32_t flow_unit_base(const GcmArgs& a, uint32_t u, uint32_t& r, uint32_t& i,
+                                                  uint32_t& steps) {
+  const int32_t nx = (int32_t)a.nb + 1, C = 64 * (int32_t)a.S;
+  r = u / a.nch;
+  i = u - r * a.nch;
+  steps = i == 0u ? (a.r0 + 63u) >> 6 : a.S;
+  return i == 0u ? (int32_t)a.r0 - 64 * (int32_t)steps : nx - (int32_t)(a.nch - i) * C;
+}
+__device__ __forceinline__ bool flow_full_blk(const GcmArgs& a, int32_t p, uint32_t rem) {
+  return p >= 0 && p < (int32_t)a.nb && (p + 1 < (int32_t)a.nb || rem == 16u);
+}
+// X block of step k for this lane (full data blocks only; others load a harmless block 0)
+__device__ __forceinline__ u32x4 flow_load_x(const GcmArgs& a, const uint8_t* in_rec, int32_t base, uint32_t k,
+                                             uint32_t rem) {
+  const int32_t p = base + 64 * (int32_t)k + (int32_t)(threadIdx.x & 63u);
+  return ld_blk(in_rec + 16u * (uint32_t)(flow_full_blk(a, p, rem) ? p : 0));
+}
+
+// One wavefront's unit: AES-CTR of its X positions (ciphertext / plaintext stored), Horner in
+// H^64 per lane, the radix-4 lane tree, and the chunk weight (host-keyed: H^(1 + (nch-1-i)C) from
+// a.chw, E_K(J0) folded into chunk 0) or V·H (device-keyed: E_K(J0) to a.ekj0).  va, vb: the
+// unit's first two input rows when `pre` (requested before the table staging).  Returns the
+// weighted partial (every lane), r = the unit's record.
+template <bool DECRYPT, bool DK>
+__device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk, const RowLanes& rl, u32x4 lenblk,
+                                           uint32_t u, bool pre, u32x4 va, u32x4 vb, uint32_t& r) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nb = a.nb;
+  const int32_t nx = (int32_t)nb + 1;
+  const uint32_t rem = a.len - 16u * (nb ? nb - 1u : 0u);
+  uint32_t i, steps;
+  const int32_t base = flow_unit_base(a, u, r, i, steps);
+  const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
+  uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
+  uint32_t n0, n1, n2;
+  gcm_nonce(a, r, !DECRYPT && i == 0u && lane == 0u, n0, n1, n2);
+  auto prefetch = [&](uint32_t k) -> u32x4 { return flow_load_x(a, in_rec, base, k, rem); };
+  CtrCache cc;
+  uint32_t cc_win = 0xffffffffu;
+  auto keystream = [&](uint32_t ctr) -> u32x4 {
+    const uint32_t w3 = __builtin_bswap32(ctr);
+    if ((ctr >> 8) != cc_win) {
+      ctr_cache_fill(rk, rl, n0, n1, n2, w3, cc);
+      cc_win = ctr >> 8;
+    }
+    uint32_t s0, s1, s2, s3;
+    aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
+    return u32x4{s0, s1, s2, s3};
+  };
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  auto consume_ks = [&](uint32_t k, u32x4 v, u32x4 ks) {
+    const int32_t p = base + 64 * (int32_t)k + (int32_t)lane;
+    u32x4 x = {0u, 0u, 0u, 0u};
+    if (p >= 0 && p < (int32_t)nb) {
+      uint8_t* op = out_rec + 16u * (uint32_t)p;
+      if (flow_full_blk(a, p, rem)) {
+        const u32x4 o = v ^ ks;
+        st_blk(op, o);
+        x = DECRYPT ? v : o;
+      } else {
+        const u32x4 pp = load_partial(in_rec + 16u * (uint32_t)p, rem);
+        const u32x4 o = mask_bytes(pp ^ ks, rem);
+        store_partial(op, o, rem);
+        x = DECRYPT ? pp : o;
+      }
+    } else if (p == nx - 1) {
+      x = lenblk;
+    }
+    if (k == 0u) acc = x;  // wave-uniform; acc was 0
+    else acc = gmul_nib(acc, flow_tab(9u)) ^ x;
+  };
+  auto ctr_of = [&](uint32_t k) { return 2u + (uint32_t)(base + 64 * (int32_t)k + (int32_t)lane); };
+  if (!pre) {
+    va = prefetch(0);
+    vb = prefetch(1);
+  }
+  uint32_t it = 0;
+  // E_K(J0), folded into chunk 0's partial (only lane 0's copy is used).  Chunk 0 holds the
+  // r0 = G..2G-1 leading positions, so its first step is partial whenever 64 does not divide
+  // r0 (1 MiB: 257 positions, lane 63 alone): lane 0 is idle there and encrypts J0 in that
+  // step instead of the wave paying a whole AES pass for it afterwards.
+  const bool j0_step0 = i == 0u && base < 0;
+  u32x4 ekj = {0u, 0u, 0u, 0u};
+  for (uint32_t k = 0; k < steps; k += 2u) {
+    rotate_prio(it++);
+    const u32x4 ks = keystream(k == 0u && j0_step0 && lane == 0u ? 1u : ctr_of(k));
+    if (k == 0u) ekj = ks;
+    consume_ks(k, va, ks);
+    va = prefetch(k + 2u);
+    if (k + 1u < steps) consume_ks(k + 1u, vb, keystream(ctr_of(k + 1u)));
+    vb = prefetch(k + 3u);
+  }
+  if (!j0_step0) ekj = i == 0u ? keystream(1u) : u32x4{0u, 0u, 0u, 0u};
+  if (pre) CMPI_PROBE(a, 2u);
+  u32x4 V = flow_tree_r4(acc, lane);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) V[c] = (uint32_t)__builtin_amdgcn_readfirstlane(V[c]);
+  u32x4 pw;
+  if constexpr (!DK) {
+    pw = gmul_wave(V, a.chw[4u * i + 3u]) ^ ekj;  // H^(1 + (nch-1-i)C) · V, E_K(J0) in chunk 0
+  } else {  // device-keyed: V · H here, H^((nch-1-i)C) and E_K(J0) in gcm_combine_kernel
+    pw = gmul_nib(V, flow_tab(0u));
+    if (i == 0u && lane == 0u) a.ekj0[r] = ekj;
+  }
+  if (pre) CMPI_PROBE(a, 5u);
+  return pw;
+}
+
 template <bool DECRYPT, int NT, bool DK>
 __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
   CMPI_PROBE(a, 0u);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t nb = a.nb;
-  const int32_t nx = (int32_t)nb + 1;
   const uint32_t rem = a.len - 16u * (nb ? nb - 1u : 0u);
-  const int32_t C = 64 * (int32_t)a.S;
   constexpr uint32_t wpb = NT / 64;
   const uint32_t units = a.nrec * a.nch;
-  // unit u = (record r, chunk i): chunk 0 absorbs the remainder, the others are C X-blocks
-  auto unit_base = [&](uint32_t u, uint32_t& r, uint32_t& i, uint32_t& steps) -> int32_t {
-    r = u / a.nch;
-    i = u - r * a.nch;
-    steps = i == 0u ? (a.r0 + 63u) >> 6 : a.S;
-    return i == 0u ? (int32_t)a.r0 - 64 * (int32_t)steps : nx - (int32_t)(a.nch - i) * C;
-  };
-  auto full_blk = [&](int32_t p) { return p >= 0 && p < (int32_t)nb && (p + 1 < (int32_t)nb || rem == 16u); };
-  auto load_x = [&](const uint8_t* in_rec, int32_t base, uint32_t k) -> u32x4 {
-    const int32_t p = base + 64 * (int32_t)k + (int32_t)lane;
-    return ld_blk(in_rec + 16u * (uint32_t)(full_blk(p) ? p : 0));
-  };
   // the first unit's first two input rows are requested before the table staging: their HBM
   // latency overlaps it
   u32x4 va0 = {0u, 0u, 0u, 0u}, vb0 = {0u, 0u, 0u, 0u};
@@ -436,9 +533,9 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
     const uint32_t u = blockIdx.x * wpb + wv;
     if (u < units) {
       uint32_t r, i, steps;
-      const int32_t base = unit_base(u, r, i, steps);
-      va0 = load_x(a.in + (uint64_t)r * a.in_stride, base, 0u);
-      vb0 = load_x(a.in + (uint64_t)r * a.in_stride, base, 1u);
+      const int32_t base = flow_unit_base(a, u, r, i, steps);
+      va0 = flow_load_x(a, a.in + (uint64_t)r * a.in_stride, base, 0u, rem);
+      vb0 = flow_load_x(a, a.in + (uint64_t)r * a.in_stride, base, 1u, rem);
     }
   }
   stage_flow<NT>(a);
@@ -451,80 +548,8 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
     const uint32_t u = ub + wv;
     u32x4 pw = {0u, 0u, 0u, 0u};
     uint32_t r = 0xffffffffu;
-    if (u < units) {  // wave-uniform
-      uint32_t i, steps;
-      const int32_t base = unit_base(u, r, i, steps);
-      const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
-      uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
-      uint32_t n0, n1, n2;
-      gcm_nonce(a, r, !DECRYPT && i == 0u && lane == 0u, n0, n1, n2);
-      auto prefetch = [&](uint32_t k) -> u32x4 { return load_x(in_rec, base, k); };
-      CtrCache cc;
-      uint32_t cc_win = 0xffffffffu;
-      auto keystream = [&](uint32_t ctr) -> u32x4 {
-        const uint32_t w3 = __builtin_bswap32(ctr);
-        if ((ctr >> 8) != cc_win) {
-          ctr_cache_fill(rk, rl, n0, n1, n2, w3, cc);
-          cc_win = ctr >> 8;
-        }
-        uint32_t s0, s1, s2, s3;
-        aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
-        return u32x4{s0, s1, s2, s3};
-      };
-      u32x4 acc = {0u, 0u, 0u, 0u};
-      auto consume_ks = [&](uint32_t k, u32x4 v, u32x4 ks) {
-        const int32_t p = base + 64 * (int32_t)k + (int32_t)lane;
-        u32x4 x = {0u, 0u, 0u, 0u};
-        if (p >= 0 && p < (int32_t)nb) {
-          uint8_t* op = out_rec + 16u * (uint32_t)p;
-          if (full_blk(p)) {
-            const u32x4 o = v ^ ks;
-            st_blk(op, o);
-            x = DECRYPT ? v : o;
-          } else {
-            const u32x4 pp = load_partial(in_rec + 16u * (uint32_t)p, rem);
-            const u32x4 o = mask_bytes(pp ^ ks, rem);
-            store_partial(op, o, rem);
-            x = DECRYPT ? pp : o;
-          }
-        } else if (p == nx - 1) {
-          x = lenblk;
-        }
-        if (k == 0u) acc = x;  // wave-uniform; acc was 0
-        else acc = gmul_nib(acc, flow_tab(9u)) ^ x;
-      };
-      auto ctr_of = [&](uint32_t k) { return 2u + (uint32_t)(base + 64 * (int32_t)k + (int32_t)lane); };
-      const bool first = ub == blockIdx.x * wpb;
-      u32x4 va = first ? va0 : prefetch(0), vb = first ? vb0 : prefetch(1);
-      uint32_t it = 0;
-      // E_K(J0), folded into chunk 0's partial (only lane 0's copy is used).  Chunk 0 holds the
-      // r0 = G..2G-1 leading positions, so its first step is partial whenever 64 does not divide
-      // r0 (1 MiB: 257 positions, lane 63 alone): lane 0 is idle there and encrypts J0 in that
-      // step instead of the wave paying a whole AES pass for it afterwards.
-      const bool j0_step0 = i == 0u && base < 0;
-      u32x4 ekj = {0u, 0u, 0u, 0u};
-      for (uint32_t k = 0; k < steps; k += 2u) {
-        rotate_prio(it++);
-        const u32x4 ks = keystream(k == 0u && j0_step0 && lane == 0u ? 1u : ctr_of(k));
-        if (k == 0u) ekj = ks;
-        consume_ks(k, va, ks);
-        va = prefetch(k + 2u);
-        if (k + 1u < steps) consume_ks(k + 1u, vb, keystream(ctr_of(k + 1u)));
-        vb = prefetch(k + 3u);
-      }
-      if (!j0_step0) ekj = i == 0u ? keystream(1u) : u32x4{0u, 0u, 0u, 0u};
-      if (first) CMPI_PROBE(a, 2u);
-      u32x4 V = flow_tree_r4(acc, lane);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) V[c] = (uint32_t)__builtin_amdgcn_readfirstlane(V[c]);
-      if constexpr (!DK) {
-        pw = gmul_wave(V, a.chw[4u * i + 3u]) ^ ekj;  // H^(1 + (nch-1-i)C) · V, E_K(J0) in chunk 0
-      } else {  // device-keyed: V · H here, H^((nch-1-i)C) and E_K(J0) in gcm_combine_kernel
-        pw = gmul_nib(V, flow_tab(0u));
-        if (i == 0u && lane == 0u) a.ekj0[r] = ekj;
-      }
-      if (first) CMPI_PROBE(a, 5u);
-    }
+    if (u < units)  // wave-uniform
+      pw = flow_unit<DECRYPT, DK>(a, rk, rl, lenblk, u, ub == blockIdx.x * wpb, va0, vb0, r);
     if (DK || !a.one_wg) {  // partials for the combine launch
       if (u < units && lane == 0u) a.partial[u] = pw;
       continue;

@@ -1,0 +1,226 @@
+// service_host.hpp — host side of the resident message service (service_kernels.hpp), included by
+// cmpi_aead.hip.  Opt-in per context (cmpi_service_start): single GCM messages from host memory
+// (cmpi_gcm_seal_host / _open_host with nrec = 1, len <= kSvcMaxLen) are posted to the running
+// service kernel instead of launching the direct path's kernel; the host spins on a page-locked
+// word the kernel writes.  The kernel exits after `idle_us` without messages (the CUs are
+// returned) and is relaunched by the next message.  No CPU cipher on any path: a service that
+// cannot start fails the call.
+
+#include "../../include/cmpi_service.h"
+#include "service_kernels.hpp"
+
+namespace {
+
+constexpr size_t kSvcMaxLen = (size_t)512 << 10;  // 64 chunks of 8 steps
+constexpr uint64_t kSvcLifeUs = 100000;           // relaunched at least every 100 ms
+
+struct Svc {
+  hipStream_t st = nullptr;
+  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..15], done [32..35]
+  uint32_t* dw = nullptr;      // its device address
+  uint32_t* go = nullptr;      // device control words (64 B), counter (at +64), partials (at +128)
+  cmpi::dev::u32x4* wts = nullptr;  // device chunk weights (4 x 64 x 4 blocks)
+  bool wts_ok = false;
+  uint8_t* bounce = nullptr;   // page-locked: pageable messages
+  size_t bcap = 0;
+  uint32_t seq = 0;            // last seq posted
+  uint32_t gen = 0;            // generation of the last launch
+  bool running = false;
+  uint32_t idle_us = 2000;
+  uint32_t* ring() { return hw; }
+  uint32_t* done() { return hw + 32; }
+};
+
+void svc_release(Svc& S) {
+  if (S.st) (void)hipStreamDestroy(S.st);
+  if (S.hw) (void)hipHostFree(S.hw);
+  if (S.go) (void)hipFree(S.go);
+  if (S.wts) (void)hipFree(S.wts);
+  if (S.bounce) (void)hipHostFree(S.bounce);
+  S = Svc{};
+}
+
+// H^(1 + (63-k)·64·2^s) at wts[256s + 4k + 3] (the flow kernel's chunk-weight slot layout)
+int svc_weights(const cmpi_ctx* c, Svc& S) {
+  std::vector<Blk> w(4 * 64 * 4);
+  for (uint32_t s = 0; s < 4; ++s) {
+    const Blk P = cmpi::gf_pow(c->H, 64u << s);
+    Blk wi = c->H;  // k = 63 down to 0
+    for (uint32_t k = 64; k-- > 0;) {
+      w[256 * s + 4 * k + 3] = wi;
+      wi = cmpi::gf_mul(wi, P);
+    }
+  }
+  HIP_TRY(hipMemcpy(S.wts, w.data(), w.size() * sizeof(Blk), hipMemcpyHostToDevice));
+  S.wts_ok = true;
+  return CMPI_OK;
+}
+
+int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
+  if (!S.wts_ok)
+    if (int rc = svc_weights(c, S)) return rc;
+  int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_service_kernel), c->device, cmpi::dev::kFlowLds);
+  if (rc) return rc;
+  if ((rc = wait_keys(c, S.st))) return rc;  // tables of a re-key still in flight on the caller's stream
+  cmpi::dev::SvcArgs a{};
+  a.ring = S.dw;
+  a.done = S.dw + 32;
+  a.go = S.go;
+  a.cnt = S.go + 16;
+  a.part = reinterpret_cast<cmpi::dev::u32x4*>(S.go + 32);
+  a.wts = S.wts;
+  a.te0 = c->dt->te0;
+  a.wtab = reinterpret_cast<const cmpi::dev::u32x4*>(c->dt->fnib[0]);
+  a.seq0 = seq0;
+  a.gen = ++S.gen;
+  a.idle_ticks = (uint64_t)S.idle_us * 100u;
+  a.life_ticks = kSvcLifeUs * 100u;
+  a.cap_ticks = (kSvcLifeUs + 100000u) * 100u;
+  a.rk = folded(c->rk);
+  HIP_TRY(hipMemsetAsync(S.go + 16, 0, 4, S.st));  // arrival counter
+  void* kargs[] = {&a};
+  HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(cmpi::dev::gcm_service_kernel), dim3(cmpi::dev::kSvcGroups),
+                          dim3(cmpi::dev::kSvcThreads), kargs, cmpi::dev::kFlowLds, S.st));
+  S.running = true;
+  return CMPI_OK;
+}
+
+// The current generation has exited (idle, lifetime, stop): its exit word is written.
+bool svc_exited(Svc& S) { return __atomic_load_n(S.done() + 2, __ATOMIC_ACQUIRE) == S.gen; }
+
+// Stop a running service and drain its stream (ctx free, re-key, cmpi_service_stop).  hmu held.
+int svc_stop_locked(Svc& S) {
+  if (!S.st) return CMPI_OK;
+  if (S.running && !svc_exited(S)) {
+    uint32_t* r = S.ring();
+    r[1] = cmpi::dev::kSvcStop;
+    __atomic_store_n(r, ++S.seq, __ATOMIC_RELEASE);
+  }
+  HIP_TRY(hipStreamSynchronize(S.st));  // the kernel exits at its next poll
+  S.running = false;
+  return CMPI_OK;
+}
+
+// Stop and free the context's service (hmu held).
+int svc_shutdown_locked(cmpi_ctx* c) {
+  if (!c->svc) return CMPI_OK;
+  const int rc = svc_stop_locked(*c->svc);
+  svc_release(*c->svc);
+  delete c->svc;
+  c->svc = nullptr;
+  return rc;
+}
+
+// One message through the service.  hmu held; pageable buffers go through the bounce.
+template <bool DEC>
+int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const uint8_t* nonce, size_t len,
+             int32_t* status) {
+  const size_t in_rec = len + (DEC ? 16 : 0), out_rec = len + (DEC ? 0 : 16);
+  void* din = in_rec ? pinned_dev_ptr(in) : nullptr;
+  void* dout = pinned_dev_ptr(out);
+  uint8_t* hout = nullptr;
+  const size_t bi = (in_rec + 255) & ~(size_t)255, need = bi + out_rec + 256;
+  if ((!din || !dout) && S.bcap < need) {
+    if (S.bounce) (void)hipHostFree(S.bounce);
+    S.bounce = nullptr;
+    S.bcap = 0;
+    const size_t cap = std::max<size_t>(need, (size_t)1 << 20);
+    if (hipHostMalloc((void**)&S.bounce, cap, hipHostMallocDefault) != hipSuccess)
+      return fail(CMPI_ENOMEM, "hipHostMalloc service bounce failed");
+    S.bcap = cap;
+  }
+  if (!din) {
+    if (in_rec) memcpy(S.bounce, in, in_rec);
+    din = pinned_dev_ptr(S.bounce);
+  }
+  if (!dout) {
+    hout = S.bounce + bi;
+    dout = pinned_dev_ptr(hout);
+  }
+  if (!din || !dout) return fail(CMPI_EHIP, "service buffers have no device address");
+  if (S.running && svc_exited(S)) {  // idled out since the last message
+    HIP_TRY(hipStreamSynchronize(S.st));
+    S.running = false;
+  }
+  if (!S.running)
+    if (int rc = svc_launch(c, S, S.seq)) return rc;
+  uint32_t* r = S.ring();
+  r[1] = DEC ? cmpi::dev::kSvcOpen : cmpi::dev::kSvcSeal;
+  r[2] = (uint32_t)len;
+  r[3] = (uint32_t)(uintptr_t)din;
+  r[4] = (uint32_t)((uintptr_t)din >> 32);
+  r[5] = (uint32_t)(uintptr_t)dout;
+  r[6] = (uint32_t)((uintptr_t)dout >> 32);
+  memcpy(r + 7, nonce, 12);
+  const uint32_t seq = ++S.seq;
+  __atomic_store_n(r, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  int relaunches = 0;
+  for (uint32_t i = 1;; ++i) {
+    if (__atomic_load_n(S.done(), __ATOMIC_ACQUIRE) == seq) break;
+    if (svc_exited(S)) {  // the generation ended (lifetime): let every workgroup finish first
+      HIP_TRY(hipStreamSynchronize(S.st));
+      S.running = false;
+      if (__atomic_load_n(S.done(), __ATOMIC_ACQUIRE) == seq) break;
+      if (++relaunches > 2) return fail(CMPI_EHIP, "message service did not complete message %u", seq);
+      if (int rc = svc_launch(c, S, seq - 1)) return rc;  // it never saw the message
+      continue;
+    }
+    if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+      const hipError_t e = hipStreamQuery(S.st);
+      if (e != hipSuccess && e != hipErrorNotReady) return fail(CMPI_EHIP, "service kernel: %s", hipGetErrorString(e));
+      if (e == hipSuccess && __atomic_load_n(S.done(), __ATOMIC_ACQUIRE) != seq && !svc_exited(S))
+        return fail(CMPI_EHIP, "service kernel ended without completing message %u", seq);
+    }
+  }
+  const int32_t ok = (int32_t)__atomic_load_n(S.done() + 1, __ATOMIC_ACQUIRE);
+  if (hout) memcpy(out, hout, out_rec);
+  if (DEC) {
+    if (status) *status = ok;
+    if (ok != 1) return fail(CMPI_EAUTH, "1 of 1 records failed authentication");
+  }
+  return CMPI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  if (c->alg != CMPI_AES_128_GCM) return fail(CMPI_EINVAL, "the message service serves AES-128-GCM contexts");
+  if (c->dev_keys) return fail(CMPI_EINVAL, "the message service needs a host-keyed context");
+  DeviceGuard dg(c->device);
+  std::lock_guard<std::mutex> lk(c->hmu);
+  if (!c->svc) c->svc = new Svc();
+  Svc& S = *c->svc;
+  S.idle_us = idle_us ? std::min<uint32_t>(idle_us, 1000000u) : 2000u;
+  if (S.st) return CMPI_OK;
+  if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void**)&S.hw, 256, hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&S.dw, S.hw, 0) != hipSuccess || hipMalloc((void**)&S.go, 256) != hipSuccess ||
+      hipMalloc((void**)&S.wts, 4 * 64 * 4 * 16) != hipSuccess || hipMemset(S.go, 0, 256) != hipSuccess) {
+    svc_release(S);
+    delete c->svc;
+    c->svc = nullptr;
+    return fail(CMPI_EHIP, "message service allocation failed");
+  }
+  memset(S.hw, 0, 256);
+  return CMPI_OK;
+}
+
+int cmpi_service_stop(cmpi_ctx* c) {
+  if (!c) return fail(CMPI_EINVAL, "null ctx");
+  DeviceGuard dg(c->device);
+  std::lock_guard<std::mutex> lk(c->hmu);
+  if (!c->svc) return CMPI_OK;
+  return svc_shutdown_locked(c);
+}
+
+int cmpi_service_running(const cmpi_ctx* c) {
+  if (!c) return 0;
+  std::lock_guard<std::mutex> lk(c->hmu);
+  return c->svc && c->svc->running && !svc_exited(*c->svc) ? 1 : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,252 @@
+// service_kernels.hpp — resident message service for single GCM messages from host memory
+// (gfx950).  The per-message EVP path (EVP_AEAD_CTX_seal / _open once per MPI message,
+// send.c:294-315, recv.c:322) pays a kernel launch, the table staging and the host's completion
+// wait on every message; this kernel is launched once, keeps the flow kernel's tables in LDS and
+// serves messages posted in a page-locked host ring until it has been idle for `idle_ticks`
+// (or has lived `life_ticks`): then it exits and the host relaunches it on the next message.
+//
+// Protocol (one message in flight per context; service_host.hpp is the host side):
+//   host:   descriptor words ring[1..9] (op, len, in, out, nonce), then ring[0] = seq (release).
+//   leader (workgroup 0, one lane): polls ring[0] with system-scope loads; on a new seq copies the
+//           descriptor to device memory (go[4..12], write-through) and publishes go[1] = seq;
+//           on idle / lifetime / op STOP it publishes go[2] = 1, writes done[2] = gen and exits.
+//   others: poll go[] (write-through loads), run their share, exit on go[2].
+//   message: the flow decomposition (gcm_flow_kernel's unit code): chunks of C = 64·S X-blocks,
+//           S the smallest power of two <= 8 with at most 64 chunks, one wavefront per chunk,
+//           8 chunks per workgroup; every chunk's partial is weighted by H^(1 + (nch-1-i)C) (host
+//           precomputed for the four S) and chunk 0 holds E_K(J0), so the tag is the XOR of the
+//           partials.  A workgroup XORs its waves' partials; with several workgroups each
+//           publishes its partial write-through, writes its L2 back to the host (system release)
+//           and adds to an arrival counter — the last arriver XORs the partials
+//           (MI355X_MICROARCH.md, Valid forms: sc1 16-B stores, agent add, sc1 loads by the adder
+//           whose add came last), writes the tag (seal) or checks it (open; zero-fills a forged
+//           message, aead.h:276-278), resets the counter and writes done[1] = status, done[0] =
+//           seq with a system-scope release.
+// Every wave's wait loop is bounded by the wall clock: the grid drains even if the host vanishes.
+#pragma once
+#include "gcm_kernels.hpp"
+
+namespace cmpi {
+namespace dev {
+
+constexpr uint32_t kSvcThreads = 512u;
+constexpr uint32_t kSvcGroups = 8u;      // workgroups (one per XCD when the chip is free)
+constexpr uint32_t kSvcMaxChunks = 64u;  // kSvcGroups x 8 waves
+constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u;
+constexpr uint32_t kSvcDesc = 9u;  // descriptor words: op, len, in lo/hi, out lo/hi, nonce[3]
+
+struct SvcArgs {
+  const uint32_t* ring;  // page-locked host words (device address): [0] posted seq, [1..9] descriptor
+  uint32_t* done;        // page-locked host words: [0] completed seq, [1] status, [2] exited generation
+  uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [4..12] descriptor copy
+  uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
+  u32x4* part;           // device: one partial per workgroup
+  const u32x4* wts;      // device: 4 x 64 x 4; wts[256s + 4k + 3] = H^(1 + (63-k)·64·2^s)
+  const uint32_t* te0;
+  const u32x4* wtab;     // the ten flow nibble tables (DevTables::fnib)
+  uint32_t seq0;         // last seq consumed before this launch
+  uint32_t gen;
+  uint64_t idle_ticks, life_ticks, cap_ticks;  // 100 MHz wall clock
+  RoundKeys rk;
+};
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t wt_load(const uint32_t* p) {  // write-through word (sc1)
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wt_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16 B published for other workgroups (two 8-B write-through stores) / read back
+__device__ __forceinline__ void wt_store16(u32x4* p, u32x4 v) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p);
+  __hip_atomic_store(q, (uint64_t)v[0] | ((uint64_t)v[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, (uint64_t)v[2] | ((uint64_t)v[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u32x4 wt_load16(const u32x4* p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+  const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// LDS words shared by the workgroup (inside the flow aggregation area)
+constexpr uint32_t kSvcX = kFlowAgg + 256u;  // [0] exit, [1] seq, [2..10] descriptor, [11] last, [12] ok
+constexpr uint32_t kSvcTag = kFlowAgg + 128u;  // the XOR of the partials (16 B)
+
+template <bool DECRYPT>
+__device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl, uint32_t seq) {
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, wg = blockIdx.x;
+  constexpr uint32_t wpb = kSvcThreads / 64u;
+  const uint32_t len = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 12u));
+  uint8_t* inp = reinterpret_cast<uint8_t*>(((uint64_t)__builtin_amdgcn_readfirstlane(lds32(kSvcX + 20u)) << 32) |
+                                            __builtin_amdgcn_readfirstlane(lds32(kSvcX + 16u)));
+  uint8_t* outp = reinterpret_cast<uint8_t*>(((uint64_t)__builtin_amdgcn_readfirstlane(lds32(kSvcX + 28u)) << 32) |
+                                             __builtin_amdgcn_readfirstlane(lds32(kSvcX + 24u)));
+  GcmArgs a{};
+  a.in = inp;
+  a.out = outp;
+  a.len = len;
+  a.nb = (len + 15u) >> 4;
+  a.nrec = 1u;
+  a.nmode = 3u;
+  a.nfix[0] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 32u));
+  a.nfix[1] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 36u));
+  a.nfix[2] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 40u));
+  const uint32_t nx = a.nb + 1u;
+  uint32_t ls = 0u;
+  while (ls < 3u && nx >= (kSvcMaxChunks + 1u) * (64u << ls)) ++ls;
+  const uint32_t C = 64u << ls;
+  const uint32_t nch = nx >= C ? nx / C : 1u;  // chunk 0: C <= r0 < 2C (or the whole message)
+  a.S = 1u << ls;
+  a.nch = nch;
+  a.r0 = nx - (nch - 1u) * C;
+  a.chw = s.wts + 256u * ls + 4u * (kSvcMaxChunks - nch);  // a.chw[4i + 3] = H^(1 + (nch-1-i)C)
+  const uint32_t ngrp = (nch + wpb - 1u) / wpb;  // workgroups with chunks
+  if (wg >= ngrp) return;
+  const uint64_t cbits = (uint64_t)len * 8u;
+  const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
+  const uint32_t u = wg * wpb + wv;
+  u32x4 pw = {0u, 0u, 0u, 0u};
+  if (u < nch) {
+    uint32_t r;
+    pw = flow_unit<DECRYPT, false>(a, s.rk, rl, lenblk, u, false, pw, pw, r);
+  }
+  if (lane == 0u) lds_st128(kFlowAgg + 16u * wv, pw);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores are performed
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    u32x4 x = lds128(kFlowAgg);
+    for (uint32_t j = 1; j < wpb; ++j) x ^= lds128(kFlowAgg + 16u * j);
+    uint32_t last = 1u;
+    if (ngrp > 1u) {
+      wt_store16(s.part + wg, x);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this XCD's L2 (the record bytes) back to the host
+      last = __hip_atomic_fetch_add(s.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngrp - 1u ? 1u : 0u;
+      if (last) {
+        x = wt_load16(s.part);
+        for (uint32_t j = 1; j < ngrp; ++j) x ^= wt_load16(s.part + j);
+      }
+    }
+    lds_st32(kSvcX + 44u, last);
+    lds_st128(kSvcTag, x);
+  }
+  __syncthreads();
+  if (!lds32(kSvcX + 44u)) return;  // workgroup-uniform
+  // the last arriver: tag / verdict, then the host word
+  if (threadIdx.x == 0u) {
+    const u32x4 tag = lds128(kSvcTag);
+    uint32_t ok = 1u;
+    if (!DECRYPT) {
+      st_blk(outp + len, tag);
+    } else {
+      const u32x4 d = ld_blk(inp + len) ^ tag;
+      ok = (d[0] | d[1] | d[2] | d[3]) == 0u ? 1u : 0u;
+    }
+    lds_st32(kSvcX + 48u, ok);
+  }
+  __syncthreads();
+  if (DECRYPT && !lds32(kSvcX + 48u)) {  // forged: zero-fill the plaintext (after every workgroup's stores)
+    const uint32_t full4 = len & ~3u;
+    for (uint32_t i = threadIdx.x * 4u; i < full4; i += kSvcThreads * 4u) *reinterpret_cast<u32a*>(outp + i) = 0u;
+    for (uint32_t i = full4 + threadIdx.x; i < len; i += kSvcThreads) outp[i] = 0u;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    if (ngrp > 1u) wt_store(s.cnt, 0u);
+    __hip_atomic_store(s.done + 1, lds32(kSvcX + 48u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(s.done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
+  {
+    GcmArgs t{};
+    t.te0 = s.te0;
+    t.wtab = s.wtab;
+    stage_flow<kSvcThreads>(t);
+  }
+  const RowLanes rl = row_lanes(kGcmRows);
+  const bool leader = blockIdx.x == 0u;
+  const uint64_t t0 = wall_clock64();
+  uint64_t t_last = t0;
+  uint32_t cur = s.seq0;
+  if (leader && threadIdx.x == 0u) {  // this generation's control words
+    wt_store(s.go + 1, cur);
+    wt_store(s.go + 2, 0u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wt_store(s.go, s.gen);
+  }
+  for (;;) {
+    if (threadIdx.x == 0u) {
+      uint32_t ex = 0u, q = cur;
+      uint32_t d[kSvcDesc] = {};
+      if (leader) {
+        for (;;) {
+          q = sys_load(s.ring);
+          if (q != cur) {
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcDesc; ++j) d[j] = sys_load(s.ring + 1u + j);
+            if (d[0] == kSvcStop) ex = 1u;
+            break;
+          }
+          const uint64_t now = wall_clock64();
+          if (now - t_last > s.idle_ticks || now - t0 > s.life_ticks) {
+            ex = 1u;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ex) {
+#pragma unroll
+          for (uint32_t j = 0; j < kSvcDesc; ++j) wt_store(s.go + 4u + j, d[j]);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          wt_store(s.go + 1, q);
+        } else {
+          wt_store(s.go + 2, 1u);
+        }
+      } else {
+        for (;;) {
+          if (wt_load(s.go) == s.gen) {
+            if (wt_load(s.go + 2)) {
+              ex = 1u;
+              break;
+            }
+            q = wt_load(s.go + 1);
+            if (q != cur) {
+#pragma unroll
+              for (uint32_t j = 0; j < kSvcDesc; ++j) d[j] = wt_load(s.go + 4u + j);
+              break;
+            }
+          }
+          if (wall_clock64() - t0 > s.cap_ticks) {  // bound: the leader exits long before this
+            ex = 1u;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
+        }
+      }
+      lds_st32(kSvcX, ex);
+      lds_st32(kSvcX + 4u, q);
+#pragma unroll
+      for (uint32_t j = 0; j < kSvcDesc; ++j) lds_st32(kSvcX + 8u + 4u * j, d[j]);
+      if (!ex) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // this CU / XCD sees the host's fresh bytes
+    }
+    __syncthreads();
+    if (lds32(kSvcX)) break;
+    const uint32_t q = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 4u));
+    const uint32_t op = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 8u));
+    if (op == kSvcOpen) svc_message<true>(s, rl, q);
+    else svc_message<false>(s, rl, q);
+    __syncthreads();  // LDS words reused by the next message
+    cur = q;
+    t_last = wall_clock64();
+  }
+  if (leader && threadIdx.x == 0u) __hip_atomic_store(s.done + 2, s.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace dev
+}  // namespace cmpi

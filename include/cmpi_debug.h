@@ -41,9 +41,10 @@ void cmpi_debug_set_flow_one_wg(int on);
 /* Host-memory calls (cmpi_*_host) up to `bytes` of input + output records run the direct path
  * (kernel on page-locked host memory, no DMA); larger ones the 3-stream pipeline.  0 = never. */
 void cmpi_debug_set_host_direct(size_t bytes);
-/* Direct host path: wait for the kernel by polling the stream (1, default) or by a blocking
- * hipStreamSynchronize (0). */
-void cmpi_debug_set_host_spin(int on);
+/* Direct host path: how the host waits for a call's kernels — 0 blocking hipStreamSynchronize,
+ * 1 spin on a host word written by hipStreamWriteValue32, 2 the same word written by a one-wave
+ * kernel, 3 polling hipStreamQuery. */
+void cmpi_debug_set_host_spin(int mode);
 /* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}; a wide plan reports
  * L = 64, nseg = chunks per record, G = X-blocks per chunk (64*steps). */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);

@@ -1,0 +1,40 @@
+/*
+ * cmpi_service.h — resident message service (opt-in, per context).
+ *
+ * CryptMPI seals and opens most point-to-point messages one at a time through the EVP API
+ * (MPI_SEC_Multi_Thread_Send_OpenMP: EVP_AEAD_CTX_seal per message, MV/src/mpi/pt2pt/send.c:294-315;
+ * the receiver's EVP_AEAD_CTX_open, recv.c:322).  On the device every such message otherwise costs
+ * a kernel launch, the staging of the tables and the host's completion wait.  With the service
+ * started, single GCM messages from host memory — cmpi_gcm_seal_host / cmpi_gcm_open_host with
+ * nrec = 1 and len <= 512 KiB, and therefore the EVP drop-in's per-message calls — are handed to a
+ * kernel that stays resident on 8 CUs with its tables in LDS, polls a page-locked request word and
+ * writes a page-locked completion word.  Outputs, statuses and errors are those of the calls it
+ * serves (bit-exact; forged messages zero-filled, CMPI_EAUTH).
+ *
+ * The kernel returns its CUs after `idle_us` microseconds without a message (0 = 2000) and at
+ * least every 100 ms; the next message relaunches it.  While it runs it occupies 8 CUs: large
+ * batches launched meanwhile on other streams share the remaining CUs.
+ * Host-keyed AES-128-GCM contexts only (CMPI_EINVAL otherwise).  cmpi_ctx_rekey and
+ * cmpi_ctx_rekey_subkey stop a running service (the next message restarts it with the new key;
+ * a device-keyed context ends the service).  cmpi_ctx_free stops it.
+ */
+#ifndef CMPI_SERVICE_H
+#define CMPI_SERVICE_H
+
+#include <stdint.h>
+
+#include "cmpi_aead.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int cmpi_service_start(cmpi_ctx *ctx, uint32_t idle_us);
+int cmpi_service_stop(cmpi_ctx *ctx);
+/* 1 while a service kernel of this context is resident, else 0. */
+int cmpi_service_running(const cmpi_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

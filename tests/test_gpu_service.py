@@ -1,0 +1,153 @@
+"""Resident message service (include/cmpi_service.h): single GCM messages from host memory —
+the per-message EVP_AEAD_CTX_seal / _open of MPI_SEC_Multi_Thread_Send/Recv_OpenMP
+(MV/src/mpi/pt2pt/send.c:294-315, recv.c:322) — served by a kernel that stays resident between
+messages.  Every byte and status against the oracle (oracle/gcm_ref.c: SP 800-38D, pinned to the
+reference's BoringSSL outputs); pinned and pageable buffers; forged tags zero-filled
+with CMPI_EAUTH (aead.h:276-278); idle exit and relaunch; re-key; several contexts at once."""
+import ctypes
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from cryptmpi_2022_amd import _native as N
+from cryptmpi_2022_amd import aead
+from cryptmpi_2022_amd.synth import splitmix64_bytes
+
+pytestmark = pytest.mark.gpu
+
+KEY = bytes(range(16))
+# 0 .. the service's 512 KiB limit (64 chunks of 8 steps) and one past it (the direct path)
+SIZES = [0, 1, 15, 16, 17, 100, 1000, 1024, 1040, 4096, 4097, 8191, 8192, 8193, 30000, 65535, 65536, 65537,
+         100000, 131072, 262144, 300001, 524288, 524289]
+
+
+def _host(n: int, pinned: bool, fill: int = 0):
+    if pinned:
+        t = torch.full((max(n, 1),), fill, dtype=torch.uint8).pin_memory()
+        return t.numpy()[:n], t
+    return np.full(max(n, 1), fill, np.uint8)[:n], None
+
+
+def _seal(ctx, out, pt, nonce: bytes, n: int):
+    nb = (ctypes.c_uint8 * 12).from_buffer_copy(nonce)
+    return N.lib().cmpi_gcm_seal_host(ctx.handle, ctypes.c_void_p(out.ctypes.data), n + 16,
+                                      ctypes.c_void_p(pt.ctypes.data), max(n, 1), nb, 12, n, 1)
+
+
+def _open(ctx, out, ct, nonce: bytes, n: int, st):
+    nb = (ctypes.c_uint8 * 12).from_buffer_copy(nonce)
+    return N.lib().cmpi_gcm_open_host(ctx.handle, ctypes.c_void_p(out.ctypes.data), max(n, 1),
+                                      ctypes.c_void_p(ct.ctypes.data), n + 16, nb, 12, n, 1,
+                                      ctypes.c_void_p(st.ctypes.data))
+
+
+@pytest.fixture
+def svc_ctx():
+    ctx = aead.AeadCtx(KEY)
+    ctx.service_start(20000)
+    yield ctx
+    ctx.service_stop()
+    ctx.close()
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_service_seal_open_vs_oracle(svc_ctx, pinned):
+    for n in SIZES:
+        pt = splitmix64_bytes(0x5E7 + n, n)
+        nonce = splitmix64_bytes(0x90 + n, 12).tobytes()
+        src, _k1 = _host(n, pinned)
+        src[:] = pt
+        ct, _k2 = _host(n + 16, pinned, fill=0xA5)
+        assert _seal(svc_ctx, ct, src, nonce, n) == N.CMPI_OK, n
+        want = oracle.gcm_seal(KEY, nonce, pt.tobytes())
+        assert ct.tobytes() == want, n
+        back, _k3 = _host(n, pinned, fill=0x3C)
+        st = np.full(1, 7, np.int32)
+        assert _open(svc_ctx, back, ct, nonce, n, st) == N.CMPI_OK, n
+        assert st[0] == 1 and back.tobytes() == pt.tobytes(), n
+        if n:  # a forged tag: status 0, plaintext zero-filled, CMPI_EAUTH
+            ct[n + 15] ^= 0x01
+            bad, _k4 = _host(n, pinned, fill=0x77)
+            st[0] = 7
+            assert _open(svc_ctx, bad, ct, nonce, n, st) == N.CMPI_EAUTH, n
+            assert st[0] == 0 and not bad.any(), n
+    assert svc_ctx.service_running()
+
+
+def test_service_message_sequence(svc_ctx):
+    """Many messages back to back, seal and open interleaved, sizes across every chunk count."""
+    rng = np.random.default_rng(11)
+    src, _k1 = _host(200000, True)
+    ct, _k2 = _host(200016, True)
+    back, _k3 = _host(200000, True)
+    st = np.zeros(1, np.int32)
+    for i in range(300):
+        n = int(rng.integers(0, 200000)) if i % 3 else int(rng.integers(0, 2048))
+        pt = splitmix64_bytes(i, n)
+        nonce = splitmix64_bytes(1000 + i, 12).tobytes()
+        src[:n] = pt
+        assert _seal(svc_ctx, ct, src, nonce, n) == N.CMPI_OK
+        assert ct[: n + 16].tobytes() == oracle.gcm_seal(KEY, nonce, pt.tobytes()), (i, n)
+        assert _open(svc_ctx, back, ct, nonce, n, st) == N.CMPI_OK and st[0] == 1
+        assert back[:n].tobytes() == pt.tobytes(), (i, n)
+
+
+def test_service_idle_exit_and_relaunch():
+    ctx = aead.AeadCtx(KEY)
+    ctx.service_start(300)  # 0.3 ms idle
+    pt = splitmix64_bytes(5, 4096)
+    nonce = bytes(12)
+    want = oracle.gcm_seal(KEY, nonce, pt.tobytes())
+    for _ in range(3):
+        assert ctx.seal(nonce, pt.tobytes()) == want
+        assert ctx.service_running()
+        time.sleep(0.05)
+        assert not ctx.service_running()  # the kernel returned its CUs
+    ctx.service_stop()
+    assert ctx.seal(nonce, pt.tobytes()) == want  # the direct path again
+    ctx.close()
+
+
+def test_service_rekey_and_free():
+    ctx = aead.AeadCtx(KEY)
+    ctx.service_start(0)
+    pt = splitmix64_bytes(9, 70000).tobytes()
+    nonce = bytes(range(12))
+    assert ctx.seal(nonce, pt) == oracle.gcm_seal(KEY, nonce, pt)
+    k2 = bytes(range(100, 116))
+    ctx.rekey(k2)
+    torch.cuda.synchronize()
+    assert ctx.seal(nonce, pt) == oracle.gcm_seal(k2, nonce, pt)  # relaunched with the new key
+    assert ctx.open(nonce, oracle.gcm_seal(k2, nonce, pt)) == pt
+    assert ctx.service_running()
+    ctx.close()  # stops the resident kernel
+
+
+def test_service_two_contexts():
+    a, b = aead.AeadCtx(KEY), aead.AeadCtx(bytes(16))
+    a.service_start(0)
+    b.service_start(0)
+    for i in range(20):
+        n = 1000 * i + 7
+        pt = splitmix64_bytes(i, n).tobytes()
+        nonce = splitmix64_bytes(50 + i, 12).tobytes()
+        assert a.seal(nonce, pt) == oracle.gcm_seal(KEY, nonce, pt)
+        assert b.seal(nonce, pt) == oracle.gcm_seal(bytes(16), nonce, pt)
+    a.close()
+    b.close()
+
+
+def test_service_refuses_other_contexts():
+    ocb = aead.AeadCtx(KEY, "aes-128-ocb")
+    with pytest.raises(N.CmpiError):
+        ocb.service_start(0)
+    ocb.close()
+    master = aead.AeadCtx(KEY)
+    sub = aead.AeadCtx.subkey602(master, bytes(range(16)))
+    with pytest.raises(N.CmpiError):
+        sub.service_start(0)
+    sub.close()
+    master.close()

@@ -1,0 +1,294 @@
+// Per-message latency breakdown at the EVP / 600 boundary, from C (no Python on the path):
+// launch floor (empty kernel + blocking sync / stream polling / kernel-written host flag), the
+// CPU cost of a launch and of the pointer queries, and the engine's single-message calls on device
+// buffers and through the host API (pinned and pageable).  Medians over `iters` calls.
+// Build: make -C tools msg_latency    Run: tools/msg_latency [iters]   (prints one JSON line)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../include/cmpi_aead.h"
+#include "../include/cmpi_debug.h"
+#include "../include/cmpi_service.h"
+
+#define CK(x)                                                                            \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                           \
+    }                                                                                    \
+  } while (0)
+#define CM(x)                                                                                  \
+  do {                                                                                         \
+    int r_ = (x);                                                                              \
+    if (r_) {                                                                                  \
+      fprintf(stderr, "%s:%d %s = %d (%s)\n", __FILE__, __LINE__, #x, r_, cmpi_last_error()); \
+      exit(1);                                                                                 \
+    }                                                                                          \
+  } while (0)
+
+__global__ void empty_kernel() {}
+
+// Writes `seq` to a page-locked host word after a system-scope release (vector store).
+__global__ void flag_kernel(unsigned* flag, unsigned seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Spins ~`us` microseconds on the 100 MHz wall clock, then optionally writes the host flag.
+__global__ void busy_kernel(unsigned us, unsigned* flag, unsigned seq) {
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < 100ull * us) __builtin_amdgcn_s_sleep(1);
+  __syncthreads();
+  if (flag && threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static double median_us(int iters, const std::function<void()>& fn) {
+  for (int i = 0; i < std::max(20, iters / 10); ++i) fn();
+  std::vector<double> t(iters);
+  for (int i = 0; i < iters; ++i) {
+    const double a = now_us();
+    fn();
+    t[i] = now_us() - a;
+  }
+  std::nth_element(t.begin(), t.begin() + iters / 2, t.end());
+  return t[iters / 2];
+}
+
+static void spin(hipStream_t s) {
+  for (;;) {
+    hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) CK(e);
+  }
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 2000;
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  std::string js = "{";
+  auto put = [&](const char* k, double v) {
+    char b[96];
+    snprintf(b, sizeof b, "%s\"%s\": %.2f", js.size() > 1 ? ", " : "", k, v);
+    js += b;
+  };
+  put("empty_launch_sync_us", median_us(iters, [&] {
+        empty_kernel<<<1, 64, 0, s>>>();
+        CK(hipStreamSynchronize(s));
+      }));
+  put("empty_launch_query_spin_us", median_us(iters, [&] {
+        empty_kernel<<<1, 64, 0, s>>>();
+        spin(s);
+      }));
+  put("launch_cpu_us", median_us(iters, [&] { empty_kernel<<<1, 64, 0, s>>>(); }));
+  CK(hipStreamSynchronize(s));
+  unsigned* hflag;
+  CK(hipHostMalloc((void**)&hflag, 64, hipHostMallocDefault));
+  *hflag = 0;
+  unsigned* dflag;
+  CK(hipHostGetDevicePointer((void**)&dflag, hflag, 0));
+  unsigned seq = 0;
+  put("flag_kernel_host_spin_us", median_us(iters, [&] {
+        ++seq;
+        flag_kernel<<<1, 64, 0, s>>>(dflag, seq);
+        while (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) != seq) {
+        }
+      }));
+  CK(hipStreamSynchronize(s));
+  put("empty_launch_writevalue_host_spin_us", median_us(iters, [&] {
+        ++seq;
+        empty_kernel<<<1, 64, 0, s>>>();
+        CK(hipStreamWriteValue32(s, dflag, seq, 0));
+        while (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) != seq) {
+        }
+      }));
+  CK(hipStreamSynchronize(s));
+  put("empty_then_flag_kernel_host_spin_us", median_us(iters, [&] {
+        ++seq;
+        empty_kernel<<<1, 64, 0, s>>>();
+        flag_kernel<<<1, 64, 0, s>>>(dflag, seq);
+        while (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) != seq) {
+        }
+      }));
+  CK(hipStreamSynchronize(s));
+  // a kernel that runs ~5 us (a single small message's seal), then each way of waiting for it
+  put("busy5_sync_us", median_us(iters, [&] {
+        busy_kernel<<<4, 256, 0, s>>>(5, nullptr, 0);
+        CK(hipStreamSynchronize(s));
+      }));
+  put("busy5_query_spin_us", median_us(iters, [&] {
+        busy_kernel<<<4, 256, 0, s>>>(5, nullptr, 0);
+        spin(s);
+      }));
+  put("busy5_inkernel_flag_us", median_us(iters, [&] {
+        ++seq;
+        busy_kernel<<<1, 256, 0, s>>>(5, dflag, seq);
+        while (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) != seq) {
+        }
+      }));
+  CK(hipStreamSynchronize(s));
+  put("busy5_writevalue_us", median_us(iters, [&] {
+        ++seq;
+        busy_kernel<<<4, 256, 0, s>>>(5, nullptr, 0);
+        CK(hipStreamWriteValue32(s, dflag, seq, 0));
+        while (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) != seq) {
+        }
+      }));
+  CK(hipStreamSynchronize(s));
+  put("busy5_flag_kernel_us", median_us(iters, [&] {
+        ++seq;
+        busy_kernel<<<4, 256, 0, s>>>(5, nullptr, 0);
+        flag_kernel<<<1, 64, 0, s>>>(dflag, seq);
+        while (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) != seq) {
+        }
+      }));
+  CK(hipStreamSynchronize(s));
+  {  // the same two flag forms on a coherent (fine-grained) host word
+    unsigned *hc_flag, *dc_flag;
+    CK(hipHostMalloc((void**)&hc_flag, 64, hipHostMallocCoherent));
+    *hc_flag = 0;
+    CK(hipHostGetDevicePointer((void**)&dc_flag, hc_flag, 0));
+    put("busy5_inkernel_flag_coherent_us", median_us(iters, [&] {
+          ++seq;
+          busy_kernel<<<1, 256, 0, s>>>(5, dc_flag, seq);
+          while (__atomic_load_n(hc_flag, __ATOMIC_ACQUIRE) != seq) {
+          }
+        }));
+    CK(hipStreamSynchronize(s));
+    put("busy5_writevalue_coherent_us", median_us(iters, [&] {
+          ++seq;
+          busy_kernel<<<4, 256, 0, s>>>(5, nullptr, 0);
+          CK(hipStreamWriteValue32(s, dc_flag, seq, 0));
+          while (__atomic_load_n(hc_flag, __ATOMIC_ACQUIRE) != seq) {
+          }
+        }));
+    CK(hipStreamSynchronize(s));
+    CK(hipHostFree(hc_flag));
+  }
+  {
+    hipEvent_t ev;
+    CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    put("empty_launch_event_query_spin_us", median_us(iters, [&] {
+          empty_kernel<<<1, 64, 0, s>>>();
+          CK(hipEventRecord(ev, s));
+          for (;;) {
+            hipError_t e = hipEventQuery(ev);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) CK(e);
+          }
+        }));
+    CK(hipEventDestroy(ev));
+  }
+  {
+    hipPointerAttribute_t at;
+    put("pointer_attributes_us", median_us(iters, [&] { (void)hipPointerGetAttributes(&at, hflag); }));
+  }
+
+  uint8_t key[16];
+  for (int i = 0; i < 16; ++i) key[i] = (uint8_t)i;
+  cmpi_ctx* c = cmpi_ctx_new(CMPI_AES_128_GCM, key, 16, 16, 0);
+  if (!c) {
+    fprintf(stderr, "cmpi_ctx_new: %s\n", cmpi_last_error());
+    return 1;
+  }
+  const size_t sizes[] = {1024, 4096, 65536};
+  const char* names[] = {"1k", "4k", "64k"};
+  uint8_t nonce[12] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12};
+  for (int si = 0; si < 3; ++si) {
+    const size_t n = sizes[si];
+    uint8_t *dp, *dc, *db, *hp, *hc, *hb;
+    CK(hipMalloc((void**)&dp, n));
+    CK(hipMalloc((void**)&dc, n + 16));
+    CK(hipMalloc((void**)&db, n));
+    CK(hipMemset(dp, 7, n));
+    CK(hipHostMalloc((void**)&hp, n, hipHostMallocDefault));
+    CK(hipHostMalloc((void**)&hc, n + 16, hipHostMallocDefault));
+    CK(hipHostMalloc((void**)&hb, n, hipHostMallocDefault));
+    std::vector<uint8_t> pp(n), pc(n + 16), pb(n);
+    for (size_t i = 0; i < n; ++i) hp[i] = pp[i] = (uint8_t)(i * 31 + 5);
+    uint8_t* dn;
+    CK(hipMalloc((void**)&dn, 16));
+    CK(hipMemcpy(dn, nonce, 12, hipMemcpyHostToDevice));
+    int32_t* dst;
+    CK(hipMalloc((void**)&dst, 4));
+    char k[96];
+    snprintf(k, sizeof k, "dev_seal_%s_us", names[si]);
+    put(k, median_us(iters, [&] {
+          CM(cmpi_gcm_seal_batch(c, dc, n + 16, dp, n, dn, 12, n, 1, nullptr, s));
+          spin(s);
+        }));
+    snprintf(k, sizeof k, "dev_open_%s_us", names[si]);
+    put(k, median_us(iters, [&] {
+          CM(cmpi_gcm_open_batch(c, db, n, dc, n + 16, dn, 12, n, 1, dst, nullptr, s));
+          spin(s);
+        }));
+    const char* modes[] = {"sync", "writevalue", "flagkernel", "query"};
+    for (int m = 0; m < 4; ++m) {
+      cmpi_debug_set_host_spin(m);
+      snprintf(k, sizeof k, "host_pinned_seal_%s_%s_us", names[si], modes[m]);
+      put(k, median_us(iters, [&] { CM(cmpi_gcm_seal_host(c, hc, n + 16, hp, n, nonce, 12, n, 1)); }));
+    }
+    cmpi_debug_set_host_spin(0);
+    snprintf(k, sizeof k, "host_pinned_open_%s_us", names[si]);
+    int32_t st = 0;
+    put(k, median_us(iters, [&] { CM(cmpi_gcm_open_host(c, hb, n, hc, n + 16, nonce, 12, n, 1, &st)); }));
+    if (memcmp(hb, hp, n) || st != 1) {
+      fprintf(stderr, "pinned round trip failed (%zu)\n", n);
+      return 1;
+    }
+    snprintf(k, sizeof k, "host_pageable_seal_open_%s_us", names[si]);
+    put(k, median_us(iters, [&] {
+          CM(cmpi_gcm_seal_host(c, pc.data(), n + 16, pp.data(), n, nonce, 12, n, 1));
+          CM(cmpi_gcm_open_host(c, pb.data(), n, pc.data(), n + 16, nonce, 12, n, 1, &st));
+        }));
+    if (memcmp(pb.data(), pp.data(), n) || memcmp(pc.data(), hc, n + 16)) {
+      fprintf(stderr, "pageable round trip failed (%zu)\n", n);
+      return 1;
+    }
+    // the same calls through the resident message service (include/cmpi_service.h)
+    CM(cmpi_service_start(c, 0));
+    snprintf(k, sizeof k, "svc_pinned_seal_%s_us", names[si]);
+    put(k, median_us(iters, [&] { CM(cmpi_gcm_seal_host(c, hc, n + 16, hp, n, nonce, 12, n, 1)); }));
+    snprintf(k, sizeof k, "svc_pinned_open_%s_us", names[si]);
+    put(k, median_us(iters, [&] { CM(cmpi_gcm_open_host(c, hb, n, hc, n + 16, nonce, 12, n, 1, &st)); }));
+    if (memcmp(hb, hp, n) || st != 1) {
+      fprintf(stderr, "service pinned round trip failed (%zu)\n", n);
+      return 1;
+    }
+    snprintf(k, sizeof k, "svc_pageable_seal_open_%s_us", names[si]);
+    put(k, median_us(iters, [&] {
+          CM(cmpi_gcm_seal_host(c, pc.data(), n + 16, pp.data(), n, nonce, 12, n, 1));
+          CM(cmpi_gcm_open_host(c, pb.data(), n, pc.data(), n + 16, nonce, 12, n, 1, &st));
+        }));
+    if (memcmp(pb.data(), pp.data(), n) || memcmp(pc.data(), hc, n + 16)) {
+      fprintf(stderr, "service pageable round trip failed (%zu)\n", n);
+      return 1;
+    }
+    CM(cmpi_service_stop(c));
+    CK(hipFree(dp));
+    CK(hipFree(dc));
+    CK(hipFree(db));
+    CK(hipFree(dn));
+    CK(hipFree(dst));
+    CK(hipHostFree(hp));
+    CK(hipHostFree(hc));
+    CK(hipHostFree(hb));
+  }
+  cmpi_ctx_free(c);
+  CK(hipHostFree(hflag));
+  CK(hipStreamDestroy(s));
+  printf("%s}\n", js.c_str());
+  return 0;
+}
