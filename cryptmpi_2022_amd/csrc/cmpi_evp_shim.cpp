@@ -33,6 +33,7 @@
 
 #include "../../include/cmpi_aead.h"
 #include "../../include/cmpi_evp.h"
+#include "../../include/cmpi_service.h"
 
 struct evp_aead_st {
   int id;
@@ -80,6 +81,10 @@ size_t env_size(const char* name, size_t dflt) {
 }
 const size_t kIdleCap = env_size("CMPI_EVP_CTX_CACHE", 16);
 const long kWindowUs = (long)env_size("CMPI_EVP_COALESCE_US", 30);
+// CMPI_EVP_SERVICE_US = n > 0: every context serves its single messages from the resident message
+// service (include/cmpi_service.h), which returns its CUs after n us without messages.  0 (default):
+// one kernel launch per EVP call.
+const size_t kServiceUs = env_size("CMPI_EVP_SERVICE_US", 0);
 
 int pick_device() {
   const char* vars[] = {"CMPI_DEVICE", "MV2_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK",
@@ -158,6 +163,10 @@ Shared* acquire(const uint8_t* key) {
     if (!c) return nullptr;
     s = new Shared();
     s->c = c;
+    if (kServiceUs && cmpi_service_start(c, (uint32_t)std::min<size_t>(kServiceUs, 1000000)) != CMPI_OK) {
+      destroy(s);
+      return nullptr;
+    }
   }
   s->key = k;
   s->refs = 1;

@@ -8,7 +8,9 @@
 // Protocol (one message in flight per context; service_host.hpp is the host side):
 //   host:   descriptor words ring[1..9] (op, len, in, out, nonce), then ring[0] = seq (release).
 //   leader (workgroup 0, one lane): polls ring[0] with system-scope loads; on a new seq copies the
-//           descriptor to device memory (go[4..12], write-through) and publishes go[1] = seq;
+//           descriptor to device memory (go[4..12], write-through) and publishes go[1] = seq,
+//           both under a seqlock (go[3] odd while they change: a workgroup that sat out the last
+//           message may be reading them);
 //           on idle / lifetime / op STOP it publishes go[2] = 1, writes done[2] = gen and exits.
 //   others: poll go[] (write-through loads), run their share, exit on go[2].
 //   message: the flow decomposition (gcm_flow_kernel's unit code): chunks of C = 64·S X-blocks,
@@ -38,7 +40,7 @@ constexpr uint32_t kSvcDesc = 9u;  // descriptor words: op, len, in lo/hi, out l
 struct SvcArgs {
   const uint32_t* ring;  // page-locked host words (device address): [0] posted seq, [1..9] descriptor
   uint32_t* done;        // page-locked host words: [0] completed seq, [1] status, [2] exited generation
-  uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [4..12] descriptor copy
+  uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [3] seqlock version, [4..12] descriptor copy
   uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
   u32x4* part;           // device: one partial per workgroup
   const u32x4* wts;      // device: 4 x 64 x 4; wts[256s + 4k + 3] = H^(1 + (63-k)·64·2^s)
@@ -76,15 +78,22 @@ __device__ __forceinline__ u32x4 wt_load16(const u32x4* p) {
 constexpr uint32_t kSvcX = kFlowAgg + 256u;  // [0] exit, [1] seq, [2..10] descriptor, [11] last, [12] ok
 constexpr uint32_t kSvcTag = kFlowAgg + 128u;  // the XOR of the partials (16 B)
 
+// A 64-bit address from two LDS words (lo, hi), wave-uniform.  readfirstlane returns int: each
+// word is taken as uint32_t before widening (a sign-extended low word with bit 31 set would put
+// 0xFFFFFFFF in the high half).
+__device__ __forceinline__ uint64_t lds_ptr64(uint32_t off) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane(lds32(off));
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(lds32(off + 4u));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 template <bool DECRYPT>
 __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl, uint32_t seq) {
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, wg = blockIdx.x;
   constexpr uint32_t wpb = kSvcThreads / 64u;
   const uint32_t len = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 12u));
-  uint8_t* inp = reinterpret_cast<uint8_t*>(((uint64_t)__builtin_amdgcn_readfirstlane(lds32(kSvcX + 20u)) << 32) |
-                                            __builtin_amdgcn_readfirstlane(lds32(kSvcX + 16u)));
-  uint8_t* outp = reinterpret_cast<uint8_t*>(((uint64_t)__builtin_amdgcn_readfirstlane(lds32(kSvcX + 28u)) << 32) |
-                                             __builtin_amdgcn_readfirstlane(lds32(kSvcX + 24u)));
+  uint8_t* inp = reinterpret_cast<uint8_t*>(lds_ptr64(kSvcX + 16u));
+  uint8_t* outp = reinterpret_cast<uint8_t*>(lds_ptr64(kSvcX + 24u));
   GcmArgs a{};
   a.in = inp;
   a.out = outp;
@@ -174,7 +183,9 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
   const uint64_t t0 = wall_clock64();
   uint64_t t_last = t0;
   uint32_t cur = s.seq0;
+  uint32_t ver = 0u;  // leader: the descriptor seqlock's version (go[3], even when stable)
   if (leader && threadIdx.x == 0u) {  // this generation's control words
+    ver = wt_load(s.go + 3) & ~1u;
     wt_store(s.go + 1, cur);
     wt_store(s.go + 2, 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -200,11 +211,15 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        if (!ex) {
+        if (!ex) {  // seqlock: version odd while the descriptor is rewritten
+          wt_store(s.go + 3, ++ver);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
           for (uint32_t j = 0; j < kSvcDesc; ++j) wt_store(s.go + 4u + j, d[j]);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           wt_store(s.go + 1, q);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          wt_store(s.go + 3, ++ver);
         } else {
           wt_store(s.go + 2, 1u);
         }
@@ -215,11 +230,19 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
               ex = 1u;
               break;
             }
-            q = wt_load(s.go + 1);
-            if (q != cur) {
+            // a workgroup that sat out the last message may look while the leader rewrites the
+            // descriptor for the next one: take (seq, descriptor) only from one stable version
+            const uint32_t v1 = wt_load(s.go + 3);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!(v1 & 1u)) {
+              q = wt_load(s.go + 1);
 #pragma unroll
               for (uint32_t j = 0; j < kSvcDesc; ++j) d[j] = wt_load(s.go + 4u + j);
-              break;
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              const uint32_t v2 = wt_load(s.go + 3);
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              if (v2 == v1 && q != cur) break;
+              q = cur;
             }
           }
           if (wall_clock64() - t0 > s.cap_ticks) {  // bound: the leader exits long before this

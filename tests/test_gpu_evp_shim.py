@@ -79,8 +79,9 @@ def test_ctypes_seal_open_semantics():
     L.EVP_AEAD_CTX_free(ctx)
 
 
-@pytest.mark.parametrize("threads,msgs,n", [(8, 16, 4096), (8, 4, 65536), (3, 5, 1001), (8, 2, 0)])
-def test_c_client_threads_share_one_ctx(tmp_path, threads, msgs, n):
+@pytest.mark.parametrize("threads,msgs,n,service", [(8, 16, 4096, False), (8, 4, 65536, False), (3, 5, 1001, False),
+                                                    (8, 2, 0, False), (1, 24, 4096, True), (8, 4, 65536, True)])
+def test_c_client_threads_share_one_ctx(tmp_path, threads, msgs, n, service):
     """An OpenMP-style team of pthreads sealing and opening on ONE shared EVP_AEAD_CTX through the
     drop-in (coalesced into batch launches), bit-exact vs the oracle; per-message 602 contexts
     (T x EVP_AEAD_CTX_new of a fresh key per message, pooled + re-keyed on the device); libcrypto's
@@ -97,8 +98,11 @@ def test_c_client_threads_share_one_ctx(tmp_path, threads, msgs, n):
     pt = splitmix64_bytes(0xBD, n * R)
     inp, outp = tmp_path / "in.bin", tmp_path / "out.bin"
     inp.write_bytes(key + nonces.tobytes() + pt.tobytes())
+    env = dict(os.environ)
+    if service:  # single messages served by each context's resident kernel (CMPI_EVP_SERVICE_US)
+        env["CMPI_EVP_SERVICE_US"] = "2000"
     r = subprocess.run([str(exe), str(threads), str(msgs), str(n), str(inp), str(outp)], capture_output=True,
-                       text=True, timeout=120)
+                       text=True, timeout=120, env=env)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["forwarded_aes256_ok"] == 1
