@@ -496,6 +496,114 @@ def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, wa
             "parity": "every rank's wire blocks (nonce||ct||tag) vs OpenSSL 3 EVP_aes_128_gcm seal under the wire nonces"}
 
 
+def naive_collectives_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, warmup: int = 3) -> dict:
+    """The other naive secure collectives end to end at config 5's shape (p = 8 peers of 1 MiB;
+    with fewer than 8 ranks each rank stands for 8/ranks of them, as alltoall_e2e): per call,
+    one batched seal and one batched open per rank around the stock collective on the wire blocks
+    (RCCL over xGMI; one rank: a device copy).  Root 0.
+      allgather  MPIR_Naive_Sec_Allgather (allgather.c:839-899): seal own blocks, all-gather, open 8
+      gather     approach 301 (gather.c:1508-1606): seal own blocks, gather to the root, root opens 8
+      scatter    MPIR_Naive_Sec_Scatter (scatter.c:659-730): root seals 8, scatter, open own blocks
+      bcast      MPI_Naive_Sec_Bcast (bcast.c:1510-1580): root seals 1, broadcast, the others open it
+                 (one rank: it opens its own block)
+    Every rank runs this; time = MAX over ranks; statuses checked after the timed calls."""
+    from cryptmpi_2022_amd import _native as N
+
+    p = pg.get_world_size() if pg is not None else 1
+    rank = pg.get_rank() if pg is not None else 0
+    v = -(-A2A_BLOCKS // p)  # blocks this rank stands for
+    tot = v * p
+    w = n + 28
+    dev = torch.device("cuda", device)
+    g = torch.Generator(device=dev).manual_seed(5151 + rank)
+    send = torch.randint(0, 256, (tot * n,), dtype=torch.uint8, device=dev, generator=g)
+    recv = torch.empty_like(send)
+    wire_mine = torch.empty(v * w, dtype=torch.uint8, device=dev)
+    wire_all = torch.empty(tot * w, dtype=torch.uint8, device=dev)
+    status = torch.zeros(tot, dtype=torch.int32, device=dev)
+    ctx = aead.AeadCtx(KEY, device=device)
+    ws = torch.empty(max(ctx.workspace_size(n, tot), 16), dtype=torch.uint8, device=dev)
+    L = N.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def seal(wire, src, k):
+        N.check(L.cmpi_naive_seal_blocks(ctx.handle, P(wire), P(src), n, k, P(ws), st))
+
+    def opn(dst, wire, k):
+        N.check(L.cmpi_naive_open_blocks(ctx.handle, P(dst), P(wire), n, k, P(status), P(ws), st))
+
+    def allgather():
+        seal(wire_mine, send, v)
+        if p > 1:
+            pg.all_gather_into_tensor(wire_all, wire_mine)
+        else:
+            wire_all.copy_(wire_mine)
+        opn(recv, wire_all, tot)
+        return tot
+
+    def gather():
+        seal(wire_mine, send, v)
+        if p > 1:
+            parts = list(wire_all.split(v * w)) if rank == 0 else None
+            pg.gather(wire_mine, parts, dst=0)
+        else:
+            wire_all.copy_(wire_mine)
+        if rank == 0:
+            opn(recv, wire_all, tot)
+            return tot
+        return 0
+
+    def scatter():
+        if rank == 0:
+            seal(wire_all, send, tot)
+        if p > 1:
+            pg.scatter(wire_mine, list(wire_all.split(v * w)) if rank == 0 else None, src=0)
+        else:
+            wire_mine.copy_(wire_all)
+        opn(recv, wire_mine, v)
+        return v
+
+    def bcast():
+        if rank == 0:
+            seal(wire_mine, send, 1)
+        if p > 1:
+            pg.broadcast(wire_mine[:w], src=0)
+        if rank != 0 or p == 1:
+            opn(recv, wire_mine, 1)
+            return 1
+        return 0
+
+    res = {"ranks": p, "block_bytes": n, "peers": tot, "root": 0,
+           "transport": "RCCL (xGMI)" if p > 1 else "1 rank: device copy (blocks looped back)"}
+    for name, fn in (("allgather", allgather), ("gather", gather), ("scatter", scatter), ("bcast", bcast)):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize(dev)
+        status.zero_()
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        k = 0
+        for _ in range(steps):
+            k = fn()
+        torch.cuda.synchronize(dev)
+        barrier()
+        wall = time.perf_counter() - t0
+        ok = bool((status[:k] == 1).all()) if k else True
+        if p == 1 and k:
+            ok = ok and torch.equal(recv[: k * n], send[: k * n])
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        if p > 1:
+            pg.all_reduce(t, op=pg.ReduceOp.MAX)
+            pg.all_reduce(okt, op=pg.ReduceOp.MIN)
+        res[name] = {"ms_per_call": round(float(t.item()) / steps * 1e3, 4), "blocks_opened_per_rank": k,
+                     "all_blocks_authenticated": bool(okt.item())}
+    ctx.close()
+    return res
+
+
 def config1_message(device: int, n: int = 64 << 10, iters: int = 200) -> dict:
     """BASELINE config 1's unit of work (one 64 KiB MPI_Send/MPI_Recv message, 600 framing:
     send.c:221-337 / recv.c:219-341) on this engine: per-message seal + open latency
@@ -1033,8 +1141,13 @@ def main() -> None:
         result["extras"] = extras
     if not args.no_extras:  # config 5 end to end: a collective, so every rank runs it
         a2a = alltoall_e2e(local, pg, barrier)
+        try:
+            colls = naive_collectives_e2e(local, pg, barrier)
+        except Exception as e:  # report, never hide
+            colls = {"error": repr(e)}
         if rank == 0:
             result.setdefault("extras", {})["alltoall_e2e"] = a2a
+            result["extras"]["naive_collectives_e2e"] = colls
     if rank == 0:
         print(json.dumps(result))
     if pg is not None:

@@ -406,7 +406,12 @@ __device__ __forceinline__ u32x4 flow_tree_r4(u32x4 acc, uint32_t lane) {
 // (Measured, not taken: finishing multi-workgroup batches in the same launch — chunk partials
 // published write-through, per-group arrival counters, the last workgroup XORs every record's
 // partials and zero-fills forged records, plaintext stored write-through — 8 x 1 MiB seal 30.8 vs
-// 20.8 us, 1 x 64 KiB 19.4 vs 13.4 us with the XOR-combine launch: profiles/r03d_flow_fused_ab.txt.)
+// 20.8 us, 1 x 64 KiB 19.4 vs 13.4 us with the XOR-combine launch: profiles/r03d_flow_fused_ab.txt.
+// A second form — no fences: each wave's partial stored write-through, one agent-scope add per
+// record and round, the record's last arriving workgroup XORs that record's partials, per-stream
+// zeroed counters — was also slower: 8 x 1 MiB 23.5 vs 21.1 us, 1 x 64 KiB 14.6 vs 13.4, 1 x 8 MiB
+// 24.5 vs 21.9 (profiles/r03f_flow_fused_ab.txt): store drain + add round trip + partial loads on
+// the last workgroup's path cost more than the launch boundary.)
 // Unit u = (record r, chunk i) of a flow decomposition: chunk 0 absorbs the remainder (r0 X-blocks,
 // ceil(r0/64) steps), the others are C = 64·S X-blocks; returns the base X position of lane 0's
 // first step.

@@ -12,6 +12,8 @@
 //           both under a seqlock (go[3] odd while they change: a workgroup that sat out the last
 //           message may be reading them);
 //           on idle / lifetime / op STOP it publishes go[2] = 1, writes done[2] = gen and exits.
+//           A message whose chunks fit one workgroup is served by the leader's workgroup alone
+//           and not published (the others act only on a change of go[1]).
 //   others: poll go[] (write-through loads), run their share, exit on go[2].
 //   message: the flow decomposition (gcm_flow_kernel's unit code): chunks of C = 64·S X-blocks,
 //           S the smallest power of two <= 8 with at most 64 chunks, one wavefront per chunk,
@@ -87,6 +89,17 @@ __device__ __forceinline__ uint64_t lds_ptr64(uint32_t off) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Chunk plan of a message of `len` bytes: C = 64·2^ls X-blocks per chunk, nch chunks (chunk 0
+// takes the remainder), ngrp workgroups of 8 chunks.
+__device__ __forceinline__ uint32_t svc_plan(uint32_t len, uint32_t& ls, uint32_t& nch) {
+  const uint32_t nx = ((len + 15u) >> 4) + 1u;
+  ls = 0u;
+  while (ls < 3u && nx >= (kSvcMaxChunks + 1u) * (64u << ls)) ++ls;
+  const uint32_t C = 64u << ls;
+  nch = nx >= C ? nx / C : 1u;
+  return (nch + kSvcThreads / 64u - 1u) / (kSvcThreads / 64u);
+}
+
 template <bool DECRYPT>
 __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl, uint32_t seq) {
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, wg = blockIdx.x;
@@ -105,15 +118,13 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   a.nfix[1] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 36u));
   a.nfix[2] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 40u));
   const uint32_t nx = a.nb + 1u;
-  uint32_t ls = 0u;
-  while (ls < 3u && nx >= (kSvcMaxChunks + 1u) * (64u << ls)) ++ls;
+  uint32_t ls, nch;  // chunk 0: C <= r0 < 2C (or the whole message)
+  const uint32_t ngrp = svc_plan(len, ls, nch);  // workgroups with chunks
   const uint32_t C = 64u << ls;
-  const uint32_t nch = nx >= C ? nx / C : 1u;  // chunk 0: C <= r0 < 2C (or the whole message)
   a.S = 1u << ls;
   a.nch = nch;
   a.r0 = nx - (nch - 1u) * C;
   a.chw = s.wts + 256u * ls + 4u * (kSvcMaxChunks - nch);  // a.chw[4i + 3] = H^(1 + (nch-1-i)C)
-  const uint32_t ngrp = (nch + wpb - 1u) / wpb;  // workgroups with chunks
   if (wg >= ngrp) return;
   const uint64_t cbits = (uint64_t)len * 8u;
   const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
@@ -211,7 +222,8 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        if (!ex) {  // seqlock: version odd while the descriptor is rewritten
+        uint32_t ls_, nch_;
+        if (!ex && svc_plan(d[1], ls_, nch_) > 1u) {  // seqlock: version odd while the descriptor is rewritten
           wt_store(s.go + 3, ++ver);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -220,9 +232,9 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
           wt_store(s.go + 1, q);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           wt_store(s.go + 3, ++ver);
-        } else {
+        } else if (ex) {
           wt_store(s.go + 2, 1u);
-        }
+        }  // a message of one workgroup's chunks is the leader's alone: nothing to publish
       } else {
         for (;;) {
           if (wt_load(s.go) == s.gen) {

@@ -130,5 +130,9 @@ int main(int argc, char **argv) {
   printf("{\"threads\": %d, \"msgs_per_thread\": %d, \"n\": %zu, \"team_seal_open_s\": %.6f, "
          "\"team_msgs_per_s\": %.1f, \"ctx_new_free_us_per_msg\": %.2f, \"forwarded_aes256_ok\": %d}\n",
          T, M, n, team_s, 2.0 * R / team_s, newfree_us, fwd_ok);
+  if (fwd_ok != 1) {  /* the engine's last error, for the test's failure message */
+    const char *(*lerr)(void) = (const char *(*)(void))dlsym(RTLD_DEFAULT, "cmpi_last_error");
+    fprintf(stderr, "engine: %s\n", lerr ? lerr() : "?");
+  }
   return fwd_ok == 1 ? 0 : 9;
 }

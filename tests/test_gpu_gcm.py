@@ -249,7 +249,7 @@ def test_flow_kernel_forms(threads, n, nrec, steps):
 
 def test_flow_two_streams_one_fresh_context():
     """calls on one context from two streams at once — the first use of a chunk-weight
-    table and of the fused completion's counters by either — stay correct: seals of 8 x 1 MiB and
+    table by either — stay correct: seals of 8 x 1 MiB and
     3 x 100 000 B launched back to back on two streams of a fresh context, then opened the same way."""
     import torch
 
@@ -275,6 +275,33 @@ def test_flow_two_streams_one_fresh_context():
     torch.cuda.synchronize()
     for (n, nrec, pt, *_), (back, st) in zip(data, outs):
         assert (host(st)[:nrec] == 1).all() and np.array_equal(host(back)[: nrec * n].reshape(nrec, n), pt)
+
+
+def test_flow_consecutive_shapes_one_stream():
+    """FLOW batches of changing shapes (1 to 1 500 records, 1 to 2 048 chunks each) sealed and
+    opened back to back on one stream without a synchronisation — chunk-weight tables and scratch
+    reused and grown between launches — each checked against the oracle afterwards, one forged
+    record per open."""
+    aead.force_wide(1, 0)
+    ctx = aead.AeadCtx(KEY)
+    shapes = [(70000, 2), (1 << 20, 8), (4097, 5), (70000, 2), (20000, 1500), (1 << 20, 3)]
+    jobs = []
+    for i, (n, nrec) in enumerate(shapes):
+        pt = records(0xA100 + i, nrec, n)
+        nonces = random_nonces(0xA200 + i, nrec)
+        want = oracle.gcm_seal_batch(KEY, nonces, pt)
+        forged = want.copy()
+        forged[nrec - 1, 0] ^= 0x80
+        out, back, st = empty(nrec * (n + 16), fill=0), empty(nrec * n, fill=0x55), status_buf(nrec)
+        d_n = dev(nonces)
+        ctx.seal_batch(out, dev(pt), d_n, n, nrec)
+        ctx.open_batch(back, dev(forged), d_n, n, nrec, status=st)
+        jobs.append((n, nrec, pt, want, out, back, st))
+    for n, nrec, pt, want, out, back, st in jobs:
+        assert np.array_equal(host(out)[: nrec * (n + 16)].reshape(nrec, n + 16), want), (n, nrec)
+        assert list(host(st)[:nrec]) == [1] * (nrec - 1) + [0], (n, nrec)
+        b = host(back)[: nrec * n].reshape(nrec, n)
+        assert np.array_equal(b[: nrec - 1], pt[: nrec - 1]) and not b[nrec - 1].any(), (n, nrec)
 
 
 @pytest.mark.parametrize("one_wg", [True, False])
