@@ -43,3 +43,16 @@ def golden():
     with open(os.path.join(d, "openssl_vectors.json")) as f:
         ossl = json.load(f)
     return kat, ossl
+
+
+@pytest.fixture(autouse=True)
+def _device_clean_after_gpu_test(request):
+    """A GPU test leaves the device idle and error-free: synchronise after it, so an asynchronous
+    kernel fault is reported against the test that launched the kernel, not a later one."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
