@@ -31,7 +31,6 @@ class Endpoint:
         self.cap = max_bytes
         self.send_buf = torch.empty(max_bytes + OVERHEAD, dtype=torch.uint8).pin_memory()
         self.recv_buf = torch.empty(max_bytes + OVERHEAD, dtype=torch.uint8).pin_memory()
-        self.plain = torch.empty(max(max_bytes, 1), dtype=torch.uint8).pin_memory()
         self.hdr_out = torch.zeros(HEADER, dtype=torch.uint8)
         self.hdr_in = torch.zeros(HEADER, dtype=torch.uint8)
 
@@ -49,17 +48,18 @@ class Endpoint:
         self.hdr_out.numpy()[:] = np.frombuffer(bytes(hb), np.uint8)
         sb = self.send_buf.numpy()
         sb[:12] = np.frombuffer(nonce if nonce is not None else os.urandom(12), np.uint8)  # RAND_bytes
-        src = self.plain.numpy()
-        if n:
-            src[:n] = msg.reshape(-1)
+        src = np.ascontiguousarray(msg).reshape(-1).view(np.uint8)  # sealed where it lies (MPI user buffer)
         base = self.send_buf.data_ptr()
         N.check(L.cmpi_gcm_seal_host(self.ctx.handle, ctypes.c_void_p(base + 12), n + 16,
-                                     ctypes.c_void_p(self.plain.data_ptr()), max(n, 1), ctypes.c_void_p(base), 12, n, 1))
+                                     ctypes.c_void_p(src.ctypes.data if n else base), max(n, 1),
+                                     ctypes.c_void_p(base), 12, n, 1))
         dist.send(self.hdr_out, dst, group=group)
         dist.send(self.send_buf[: n + OVERHEAD], dst, group=group)
 
-    def recv(self, src: int, group=None) -> np.ndarray:
-        """recv.c:219-341: header, payload, open; returns the plaintext (host)."""
+    def recv(self, src: int, group=None, out: np.ndarray | None = None) -> np.ndarray:
+        """recv.c:219-341: header, payload, open; returns the plaintext (host), opened straight
+        into `out` (a uint8 array of at least the message's size, the MPI receive buffer) when
+        given, else into a new array."""
         import torch.distributed as dist
 
         dist.recv(self.hdr_in, src, group=group)
@@ -68,15 +68,19 @@ class Endpoint:
         if n > self.cap:  # the header is untrusted peer input: never size a copy from it unchecked
             raise N.CmpiError(N.CMPI_EINVAL, f"peer header announces {n} B, endpoint staging holds {self.cap} B")
         dist.recv(self.recv_buf[: n + OVERHEAD], src, group=group)
+        if out is None:
+            out = np.empty(max(n, 1), np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < n:
+            raise N.CmpiError(N.CMPI_EINVAL, f"receive buffer must be a contiguous uint8 array of >= {n} bytes")
         st = ctypes.c_int32(0)
         base = self.recv_buf.data_ptr()
-        rc = N.lib().cmpi_gcm_open_host(self.ctx.handle, ctypes.c_void_p(self.plain.data_ptr()), max(n, 1),
+        rc = N.lib().cmpi_gcm_open_host(self.ctx.handle, ctypes.c_void_p(out.ctypes.data), max(n, 1),
                                         ctypes.c_void_p(base + 12), n + 16, ctypes.c_void_p(base), 12, n, 1,
                                         ctypes.byref(st))
         if rc == N.CMPI_EAUTH or st.value != 1:
             raise N.CmpiError(N.CMPI_EAUTH, "Decryption error")
         N.check(rc)
-        return self.plain.numpy()[:n].copy()
+        return out[:n]
 
     def last_payload(self, n: int) -> bytes:
         return bytes(self.send_buf.numpy()[: n + OVERHEAD])

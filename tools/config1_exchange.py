@@ -42,15 +42,17 @@ def main() -> None:
     dist.init_process_group("gloo")
     ctx = aead.AeadCtx(bytes(range(16)), device=dev)
     ep = p2p.Endpoint(ctx, max_bytes=args.msg_bytes)
-    msg = splitmix64_bytes(0xC1 + rank, args.msg_bytes)
+    # the MPI user buffers: page-locked, so the engine reads and writes them in place
+    msg = torch.from_numpy(splitmix64_bytes(0xC1 + rank, args.msg_bytes)).pin_memory().numpy()
+    rbuf = torch.empty(max(args.msg_bytes, 1), dtype=torch.uint8).pin_memory().numpy()
     peer = 1 - rank
 
     def secure_round():
         if rank == 0:
             ep.send(msg, peer)
-            got = ep.recv(peer)
+            got = ep.recv(peer, out=rbuf)
         else:
-            got = ep.recv(peer)
+            got = ep.recv(peer, out=rbuf)
             ep.send(got, peer)
         return got
 
