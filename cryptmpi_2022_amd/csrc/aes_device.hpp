@@ -229,11 +229,11 @@ __device__ __forceinline__ void aes128_dec(const RoundKeys& k, const RowLanes& L
 // Row image from a 256-word T0 (Te0 or Td0): row x = [T0[x] x32 | rotl8(T0[x]) x32].
 __device__ __forceinline__ void stage_rows(const uint32_t* __restrict__ t0, uint32_t base) {
   // entry e fills 64 words at base + 256e: 32 copies of Te0[e], then 32 of rotl8 (Te1[e]).
-  // Four threads per entry, one global load and four 16-byte LDS stores each (one pass at
-  // 1024 threads; a word-per-iteration loop paid the global-load latency 16 times).
-  for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) {
+  // Four threads per entry, one global load and four 16-byte LDS stores each; the loads of up to
+  // four passes (workgroups of >= 256 threads) are issued before any store, so a small workgroup
+  // pays one global-load latency, not four (a word-per-iteration loop paid it 16 times).
+  auto put = [&](uint32_t i, uint32_t v) {
     const uint32_t e = i >> 2, s = i & 3u;
-    uint32_t v = t0[e];
     if (s >= 2u) v = rotl8(v);
     const u32x4 q = {v, v, v, v};
     const uint32_t o = base + e * 256u + s * 64u;
@@ -241,7 +241,20 @@ __device__ __forceinline__ void stage_rows(const uint32_t* __restrict__ t0, uint
     lds_st128(o + 16u, q);
     lds_st128(o + 32u, q);
     lds_st128(o + 48u, q);
+  };
+  const uint32_t nt = blockDim.x;
+  uint32_t v[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4u; ++j) {
+    const uint32_t i = threadIdx.x + j * nt;
+    v[j] = i < 1024u ? t0[i >> 2] : 0u;
   }
+#pragma unroll
+  for (uint32_t j = 0; j < 4u; ++j) {
+    const uint32_t i = threadIdx.x + j * nt;
+    if (i < 1024u) put(i, v[j]);
+  }
+  for (uint32_t i = threadIdx.x + 4u * nt; i < 1024u; i += nt) put(i, t0[i >> 2]);
 }
 // 32-way replicated 256-word table with 128-B rows (the inverse S-box image).
 __device__ __forceinline__ void stage_rep32(const uint32_t* __restrict__ t, uint32_t base) {

@@ -50,6 +50,17 @@ __device__ __forceinline__ uint32_t gf_bit(u32x4 x, uint32_t k) {
 // maps (8 threads per i, 16 columns each); H^3 = H^2 · H by one wave (lane q holds H·x^q and
 // H·x^(q+64)); and the basis chains P · x^i of the 8 multipliers, one gf_mulx_pow per entry.
 __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
+  const uint32_t t = threadIdx.x;
+  // the 16 squaring-map columns this thread XORs for H^(2^i) depend on the key only through which
+  // of them are selected: they are requested first, so their latency overlaps the staging and
+  // the two AES encryptions below
+  u32x4 cols[16];
+  const uint32_t sq_i = 1u + (t >> 3), sq_k0 = 16u * (t & 7u);
+  if (t < 248u) {
+    const u32x4* col = a.sqmat + (sq_i - 1u) * 128u + sq_k0;
+#pragma unroll
+    for (uint32_t c = 0; c < 16u; ++c) cols[c] = col[c];
+  }
   stage_rows(a.te0, kKsRows);
   for (uint32_t x = threadIdx.x; x < 256u; x += blockDim.x) lds_st32(kKsSbox + 4u * x, (a.te0[x] >> 8) & 0xffu);
   __syncthreads();
@@ -79,7 +90,6 @@ __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
   uint32_t h0 = 0u, h1 = 0u, h2 = 0u, h3 = 0u;
   aes128_enc(fk, rl, h0, h1, h2, h3);  // H = E_K'(0^128)
   const u32x4 H = u32x4{h0, h1, h2, h3};
-  const uint32_t t = threadIdx.x;
   if (t < 44u) a.keys[t] = fk.w[t];
   if (t == 0u) {
     a.keys[48] = h0;
@@ -91,14 +101,11 @@ __global__ __launch_bounds__(256) void gcm_keysetup_kernel(KeysetupArgs a) {
   }
   // H^(2^i) = Sq^i(H) = XOR over the set bits k of H of column k of Sq^i
   if (t < 248u) {
-    const uint32_t i = 1u + (t >> 3), k0c = 16u * (t & 7u);
-    const u32x4* col = a.sqmat + (i - 1u) * 128u + k0c;
+    const uint32_t i = sq_i, k0c = sq_k0;
     u32x4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (uint32_t c = 0; c < 16u; ++c) {
-      const u32x4 v = col[c];
-      if (gf_bit(H, k0c + c)) acc ^= v;
-    }
+    for (uint32_t c = 0; c < 16u; ++c)
+      if (gf_bit(H, k0c + c)) acc ^= cols[c];
     acc ^= shfl_xor4(acc, 1);
     acc ^= shfl_xor4(acc, 2);
     acc ^= shfl_xor4(acc, 4);

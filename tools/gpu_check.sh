@@ -8,3 +8,4 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 timeout -k 10 120 tools/msg_latency 2000 > gpurun_out/msg_latency.json 2> gpurun_out/msg_latency.err || exit $?
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/gpu_tests.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
+timeout -k 10 150 python tools/framed_rates.py > gpurun_out/framed_rates.json 2> gpurun_out/framed_rates.err || exit $?
