@@ -84,6 +84,14 @@ __device__ __forceinline__ RoundKeys load_round_keys(const RoundKeys& arg, const
 
 __device__ __forceinline__ u32x4 ld_blk(const uint8_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
 __device__ __forceinline__ void st_blk(uint8_t* p, u32x4 v) { *reinterpret_cast<u32x4a*>(p) = v; }
+// Write-through (sc1) 16-byte store: the line leaves this XCD's L2 clean, so the end-of-kernel
+// write-back has nothing to write.  The FLOW kernel's record stores (few long records: the
+// launch boundary to the combine kernel is on the critical path) — 8 x 1 MiB seal 347 -> 362,
+// open 343 -> 355 GiB/s; on the lane kernel it measured neutral (1 KiB) to mixed (4 KiB seal
+// -5 %, open +3 %) and is not used there (profiles/r03j_ab_wt_stores.json).
+__device__ __forceinline__ void st_wt(uint8_t* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 // record data streamed once (MEM bit 0: loads, bit 1: stores) with the non-temporal policy
 template <int MEM>
 __device__ __forceinline__ u32x4 ld_rec(const uint8_t* p) {
@@ -472,7 +480,7 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
       uint8_t* op = out_rec + 16u * (uint32_t)p;
       if (flow_full_blk(a, p, rem)) {
         const u32x4 o = v ^ ks;
-        st_blk(op, o);
+        st_wt(op, o);
         x = DECRYPT ? v : o;
       } else {
         const u32x4 pp = load_partial(in_rec + 16u * (uint32_t)p, rem);
