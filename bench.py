@@ -1235,10 +1235,14 @@ def main() -> None:
         result["extras"] = extras
     if not args.no_extras:  # config 5 end to end: a collective, so every rank runs it
         a2a = alltoall_e2e(local, pg, barrier)
-        try:
-            colls = naive_collectives_e2e(local, pg, barrier)
-        except Exception as e:  # report, never hide
-            colls = {"error": repr(e)}
+        # the other collectives: on one rank by default (RCCL gather / scatter across ranks run
+        # only with CMPI_BENCH_COLLECTIVES=1, so a multi-GPU scaling run cannot stall on them)
+        colls = {"skipped": "multi-rank run without CMPI_BENCH_COLLECTIVES=1"}
+        if ws == 1 or os.environ.get("CMPI_BENCH_COLLECTIVES") == "1":
+            try:
+                colls = naive_collectives_e2e(local, pg, barrier)
+            except Exception as e:  # report, never hide
+                colls = {"error": repr(e)}
         if rank == 0:
             result.setdefault("extras", {})["alltoall_e2e"] = a2a
             result["extras"]["naive_collectives_e2e"] = colls
