@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of two builds of the engine on the FLOW-kernel shapes (config 5's 8 x 1 MiB,
+single 64 KiB messages, 3 x 100000 B, 1 x 8 MiB, 32 x 256 KiB).
+
+    python tools/flow_ab.py <libA.so> <libB.so> [rounds]
+
+Each (round, build) runs in its own process (`--child <lib>`): per shape, 0.3 s of warm-up, then
+seal and open kernel times from fence-free HIP events over 30 back-to-back calls; the parent prints
+per-build medians and checks that both builds produced identical ciphertext."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHAPES = {"8x1MiB": (1 << 20, 8), "1x64KiB": (65536, 1), "3x100000": (100000, 3), "1x8MiB": (8 << 20, 1),
+          "32x256KiB": (256 << 10, 32)}
+
+
+def child() -> None:
+    sys.path.insert(0, ROOT)
+    import torch
+
+    import bench
+
+    out = {}
+    for name, (n, nrec) in SHAPES.items():
+        bench.WORKLOADS["_ab"] = ("gcm", n, nrec, name)
+        w = bench.Workload("_ab", 0, seed=5)
+        st = torch.cuda.current_stream().cuda_stream
+        iters = 30
+        ev = bench.KernelEvents(2 * iters + 1)
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < 0.3:
+            for _ in range(8):
+                w.seal()
+                w.open()
+            torch.cuda.synchronize()
+        ev.record(0, st)
+        for i in range(iters):
+            w.seal()
+            ev.record(2 * i + 1, st)
+            w.open()
+            ev.record(2 * i + 2, st)
+        torch.cuda.synchronize()
+        seal = sum(ev.ms(2 * i, 2 * i + 1) for i in range(iters)) / iters * 1e3
+        opn = sum(ev.ms(2 * i + 1, 2 * i + 2) for i in range(iters)) / iters * 1e3
+        ok = w.verify()
+        out[name] = {"seal_us": seal, "open_us": opn, "ok": ok,
+                     "ct_sha": hashlib.sha256(w.ct.cpu().numpy().tobytes()).hexdigest()[:16]}
+        ev.free()
+        w.free()
+    print(json.dumps(out))
+
+
+def main() -> None:
+    if sys.argv[1] == "--child":
+        child()
+        return
+    libs = sys.argv[1:3]
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    runs = {lib: [] for lib in libs}
+    for _ in range(rounds):
+        for lib in libs:
+            env = dict(os.environ, CMPI_LIB=os.path.abspath(lib))
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib], env=env,
+                               capture_output=True, text=True, timeout=120)
+            if p.returncode != 0:
+                sys.stderr.write(p.stderr)
+                sys.exit(p.returncode)
+            runs[lib].append(json.loads(p.stdout.strip().splitlines()[-1]))
+    res = {}
+    for name in SHAPES:
+        row = {}
+        for lib in libs:
+            s = sorted(r[name]["seal_us"] for r in runs[lib])
+            o = sorted(r[name]["open_us"] for r in runs[lib])
+            n, nrec = SHAPES[name]
+            row[os.path.basename(lib)] = {"seal_us": round(s[len(s) // 2], 2), "open_us": round(o[len(o) // 2], 2),
+                                          "seal_GiBps": round(n * nrec / (s[len(s) // 2] * 1e-6) / (1 << 30), 1),
+                                          "ok": all(r[name]["ok"] for r in runs[lib])}
+        row["same_ct"] = len({r[name]["ct_sha"] for lib in libs for r in runs[lib]}) == 1
+        res[name] = row
+        print(name, row, flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
