@@ -89,8 +89,18 @@ __device__ __forceinline__ void st_blk(uint8_t* p, u32x4 v) { *reinterpret_cast<
 // launch boundary to the combine kernel is on the critical path) — 8 x 1 MiB seal 347 -> 362,
 // open 343 -> 355 GiB/s; on the lane kernel it measured neutral (1 KiB) to mixed (4 KiB seal
 // -5 %, open +3 %) and is not used there (profiles/r03j_ab_wt_stores.json).
-__device__ __forceinline__ void st_wt(uint8_t* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+// A buffer store through the builtin (aux 16 = sc1): the compiler counts it and pads its hazards.
+// (It was an inline-asm global_store_dwordx4, which hipcc schedules as an opaque instruction: in
+// a build whose schedule put a v_xor on the store's data registers right behind it, the open
+// kernel stored corrupted plaintext.)  `rec` is wave-uniform (the unit's record), off < 4 GiB.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const uint8_t* rec) {
+  const uint64_t b = (uint64_t)rec;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, -1, 0x00020000);
+}
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
 }
 // record data streamed once (MEM bit 0: loads, bit 1: stores) with the non-temporal policy
 template <int MEM>
@@ -473,6 +483,7 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
     return u32x4{s0, s1, s2, s3};
   };
   u32x4 acc = {0u, 0u, 0u, 0u};
+  const __amdgpu_buffer_rsrc_t orsrc = wt_rsrc(out_rec);
   auto consume_ks = [&](uint32_t k, u32x4 v, u32x4 ks) {
     const int32_t p = base + 64 * (int32_t)k + (int32_t)lane;
     u32x4 x = {0u, 0u, 0u, 0u};
@@ -480,7 +491,7 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
       uint8_t* op = out_rec + 16u * (uint32_t)p;
       if (flow_full_blk(a, p, rem)) {
         const u32x4 o = v ^ ks;
-        st_wt(op, o);
+        st_wt(orsrc, 16u * (uint32_t)p, o);
         x = DECRYPT ? v : o;
       } else {
         const u32x4 pp = load_partial(in_rec + 16u * (uint32_t)p, rem);
