@@ -16,7 +16,7 @@ constexpr uint64_t kSvcLifeUs = 100000;           // relaunched at least every 1
 
 struct Svc {
   hipStream_t st = nullptr;
-  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..15], done [32..35]
+  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..11] (three 16-B chunks), done [32..35]
   uint32_t* dw = nullptr;      // its device address
   uint32_t* go = nullptr;      // device control words (64 B), counter (at +64), partials (at +128)
   cmpi::dev::u32x4* wts = nullptr;  // device chunk weights (4 x 64 x 4 blocks)
@@ -30,6 +30,15 @@ struct Svc {
   uint32_t* ring() { return hw; }
   uint32_t* done() { return hw + 32; }
 };
+
+// Post descriptor d[0..8] under `seq`: chunk c = {seq, d[3c..3c+2]} at ring[4c]; the words first,
+// then seq into every chunk (the kernel takes a chunk's words only with the new seq in all three).
+void svc_post(Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc], uint32_t seq) {
+  uint32_t* r = S.ring();
+  for (uint32_t c = 0; c < 3; ++c)
+    for (uint32_t j = 0; j < 3; ++j) r[4 * c + 1 + j] = d[3 * c + j];
+  for (uint32_t c = 0; c < 3; ++c) __atomic_store_n(r + 4 * c, seq, __ATOMIC_RELEASE);
+}
 
 void svc_release(Svc& S) {
   if (S.st) (void)hipStreamDestroy(S.st);
@@ -92,9 +101,8 @@ bool svc_exited(Svc& S) { return __atomic_load_n(S.done() + 2, __ATOMIC_ACQUIRE)
 int svc_stop_locked(Svc& S) {
   if (!S.st) return CMPI_OK;
   if (S.running && !svc_exited(S)) {
-    uint32_t* r = S.ring();
-    r[1] = cmpi::dev::kSvcStop;
-    __atomic_store_n(r, ++S.seq, __ATOMIC_RELEASE);
+    const uint32_t d[cmpi::dev::kSvcDesc] = {cmpi::dev::kSvcStop};
+    svc_post(S, d, ++S.seq);
   }
   HIP_TRY(hipStreamSynchronize(S.st));  // the kernel exits at its next poll
   S.running = false;
@@ -144,16 +152,15 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
   }
   if (!S.running)
     if (int rc = svc_launch(c, S, S.seq)) return rc;
-  uint32_t* r = S.ring();
-  r[1] = DEC ? cmpi::dev::kSvcOpen : cmpi::dev::kSvcSeal;
-  r[2] = (uint32_t)len;
-  r[3] = (uint32_t)(uintptr_t)din;
-  r[4] = (uint32_t)((uintptr_t)din >> 32);
-  r[5] = (uint32_t)(uintptr_t)dout;
-  r[6] = (uint32_t)((uintptr_t)dout >> 32);
-  memcpy(r + 7, nonce, 12);
+  uint32_t d[cmpi::dev::kSvcDesc] = {DEC ? cmpi::dev::kSvcOpen : cmpi::dev::kSvcSeal,
+                                     (uint32_t)len,
+                                     (uint32_t)(uintptr_t)din,
+                                     (uint32_t)((uintptr_t)din >> 32),
+                                     (uint32_t)(uintptr_t)dout,
+                                     (uint32_t)((uintptr_t)dout >> 32)};
+  memcpy(d + 6, nonce, 12);
   const uint32_t seq = ++S.seq;
-  __atomic_store_n(r, seq, __ATOMIC_RELEASE);
+  svc_post(S, d, seq);
   const auto t0 = std::chrono::steady_clock::now();
   int relaunches = 0;
   for (uint32_t i = 1;; ++i) {

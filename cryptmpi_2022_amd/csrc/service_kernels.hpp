@@ -6,8 +6,12 @@
 // (or has lived `life_ticks`): then it exits and the host relaunches it on the next message.
 //
 // Protocol (one message in flight per context; service_host.hpp is the host side):
-//   host:   descriptor words ring[1..9] (op, len, in, out, nonce), then ring[0] = seq (release).
-//   leader (workgroup 0, one lane): polls ring[0] with system-scope loads; on a new seq copies the
+//   host:   the ring is three 16-byte chunks {seq, three descriptor words} (op, len, in, out,
+//           nonce: 9 words); the host writes the descriptor words, then seq into every chunk.
+//   leader (workgroup 0, one lane): polls the three chunks with one 16-byte system-scope load each
+//           (a 16-byte read is one snapshot of its chunk, so a chunk showing the new seq shows its
+//           new words: the descriptor arrives with the seq, no second round trip); on a new seq in
+//           all three it copies the
 //           descriptor to device memory (go[4..12], write-through) and publishes go[1] = seq,
 //           both under a seqlock (go[3] odd while they change: a workgroup that sat out the last
 //           message may be reading them);
@@ -40,7 +44,7 @@ constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u;
 constexpr uint32_t kSvcDesc = 9u;  // descriptor words: op, len, in lo/hi, out lo/hi, nonce[3]
 
 struct SvcArgs {
-  const uint32_t* ring;  // page-locked host words (device address): [0] posted seq, [1..9] descriptor
+  const uint32_t* ring;  // page-locked host words (device address): chunks [4c] = seq, [4c+1..4c+3] = desc[3c..3c+2]
   uint32_t* done;        // page-locked host words: [0] completed seq, [1] status, [2] exited generation
   uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [3] seqlock version, [4..12] descriptor copy
   uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
@@ -56,6 +60,11 @@ struct SvcArgs {
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// one 16-byte system-scope read (sc0 sc1: past every cache) of a host chunk; p wave-uniform
+__device__ __forceinline__ u32x4 sys_load16(const uint32_t* p) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p), 0, 16, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 17);
 }
 __device__ __forceinline__ uint32_t wt_load(const uint32_t* p) {  // write-through word (sc1)
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -208,10 +217,15 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
       uint32_t d[kSvcDesc] = {};
       if (leader) {
         for (;;) {
-          q = sys_load(s.ring);
+          asm volatile("" ::: "memory");  // a fresh read every pass
+          u32x4 c0 = sys_load16(s.ring), c1 = sys_load16(s.ring + 4), c2 = sys_load16(s.ring + 8);
+          asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2));  // all three reads in flight together
+          q = c0[0];
           if (q != cur) {
-#pragma unroll
-            for (uint32_t j = 0; j < kSvcDesc; ++j) d[j] = sys_load(s.ring + 1u + j);
+            if (c1[0] != q || c2[0] != q) continue;  // the host is between chunks: read again
+            d[0] = c0[1], d[1] = c0[2], d[2] = c0[3];
+            d[3] = c1[1], d[4] = c1[2], d[5] = c1[3];
+            d[6] = c2[1], d[7] = c2[2], d[8] = c2[3];
             if (d[0] == kSvcStop) ex = 1u;
             break;
           }
