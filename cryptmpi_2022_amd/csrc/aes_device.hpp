@@ -567,18 +567,6 @@ __device__ __forceinline__ u32x4 gmul_wave4(const u32x4 (&y)[4], const u32x4 (&m
 }
 
 // Partial-block helpers (bytes [0, n) of a 16-byte block at an arbitrary address).
-__device__ __forceinline__ u32x4 load_partial(const uint8_t* p, uint32_t n) {
-  uint32_t b[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) b[i] = (uint32_t)i < n ? p[i] : 0u;
-  u32x4 r;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) r[c] = b[4 * c] | (b[4 * c + 1] << 8) | (b[4 * c + 2] << 16) | (b[4 * c + 3] << 24);
-  return r;
-}
-__device__ __forceinline__ void store_partial(uint8_t* p, u32x4 v, uint32_t n) {
-  for (uint32_t i = 0; i < n; ++i) p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
-}
 __device__ __forceinline__ u32x4 mask_bytes(u32x4 v, uint32_t n) {  // keep bytes [0, n)
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -587,6 +575,24 @@ __device__ __forceinline__ u32x4 mask_bytes(u32x4 v, uint32_t n) {  // keep byte
     v[c] &= m;
   }
   return v;
+}
+// Bytes [0, n) of a block that ends a record (n <= 16), zero above.  Every byte is read from a
+// clamped address (nothing past p[n-1]) with no branch, so the 16 loads are in flight together:
+// a per-byte conditional load had the compiler wait for each one in turn (about ten memory
+// latencies in sequence per ragged record; over PCIe, for a host-memory message, ten round trips).
+__device__ __forceinline__ u32x4 load_partial(const uint8_t* p, uint32_t n) {
+  if (n == 0u) return u32x4{0u, 0u, 0u, 0u};
+  const uint32_t last = n - 1u;
+  uint32_t b[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) b[i] = p[min((uint32_t)i, last)];
+  u32x4 r;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) r[c] = b[4 * c] | (b[4 * c + 1] << 8) | (b[4 * c + 2] << 16) | (b[4 * c + 3] << 24);
+  return mask_bytes(r, n);
+}
+__device__ __forceinline__ void store_partial(uint8_t* p, u32x4 v, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
 }
 
 }  // namespace dev

@@ -297,11 +297,19 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
   if (g_force_nseg.load()) nseg = std::min<uint64_t>(g_force_nseg.load(), nx);
   // Wide decomposition (gcm_flow_kernel) when the lane-group plan leaves most of the chip idle
   // (few long records: the naive collectives' p peer blocks, 602 segments, single messages);
-  // records need >= 64 data blocks.
+  // records need >= 64 data blocks (short ones: below).
+  // Short records (under 64 data blocks), at most one round of flow waves of them: one partial
+  // step + the lane tree per record instead of a lane's nx / L serial steps (1 x 1000 B seal
+  // 32.3 -> 11.2 us, 2048 x 1000 B 52.8 -> 18.5 us, 2048 x 300 B 25.9 -> 17.4 us:
+  // profiles/r03l_flow_short_ab.json, r03l_flow_short16_ab.json).  Below 16 blocks only batches
+  // one workgroup finishes in-launch (16 x 100 B: 11.2 us on the lane kernel, 14.8 with the flow
+  // kernel's combine launch).
   const int fw = g_force_wide.load();
-  const bool wide_ok = p.nb >= 64;
-  if (wide_ok && (fw > 0 || (fw == 0 && p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target &&
-                                 (nx >= 256 || (uint64_t)nrec * p.L * nseg * 8 <= target)))) {
+  const bool short_few = p.nb >= 1 && p.nb < 64 && (p.nb >= 16 || nrec <= 8) &&
+                         (uint64_t)nrec <= (uint64_t)c->ncu * 8 && !g_force_L.load();
+  const bool wide_ok = p.nb >= 64 || short_few;
+  if (wide_ok && (fw > 0 || (fw == 0 && (short_few || (p.L == 4 && (uint64_t)nrec * p.L * nseg * 2 < target &&
+                                                        (nx >= 256 || (uint64_t)nrec * p.L * nseg * 8 <= target)))))) {
     // A round = one wave per (record, chunk) on every CU (W waves); a wave's time ~ (fixed
     // staging/weight phases) + S steps.  Chunks are cut from the end with chunk 0 absorbing the
     // remainder (G <= its length < 2G), so 1 MiB records (nx = 2^16 + 1) split into exactly

@@ -95,8 +95,28 @@ def test_batch_parity_plans(n, plan):
 
 def test_auto_plans_cover_all_lane_widths():
     ctx = aead.AeadCtx(KEY)
-    seen = {aead.gcm_plan(ctx, n, N)[0] for n, N in [(16, 1 << 20), (1024, 200000), (1024, 65536), (64, 16)]}
+    seen = {aead.gcm_plan(ctx, n, N)[0] for n, N in [(16, 1 << 20), (1024, 200000), (1024, 65536), (64, 1 << 14)]}
     assert seen == {1, 2, 4}
+
+
+@pytest.mark.parametrize("n,nrec", [(n, r) for n in (1, 15, 16, 17, 100) for r in (1, 3, 8)] +
+                         [(n, r) for n in (260, 512, 600, 1000, 1008) for r in (1, 3, 9, 100)])
+def test_short_records_flow_plan(n, nrec):
+    """Short records (< 64 data blocks), few of them: the automatic plan is the flow kernel (one
+    partial step + lane tree per record; one workgroup's batch finishes its tags in the same
+    launch, larger ones by the XOR combine): bit-exact against the oracle, round trip, a forged
+    record zero-filled."""
+    ctx = aead.AeadCtx(KEY)
+    assert aead.gcm_plan(ctx, n, nrec)[0] == 64, aead.gcm_plan(ctx, n, nrec)
+    pt = records(0x5100 + n + nrec, nrec, n)
+    nonces = random_nonces(0x5200 + n + nrec, nrec)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    assert np.array_equal(gpu_seal(ctx, nonces, pt), want)
+    forged = want.copy()
+    forged[nrec - 1, n + 3] ^= 0x10
+    back, st = gpu_open(ctx, nonces, forged)
+    assert list(st) == [1] * (nrec - 1) + [0]
+    assert np.array_equal(back[: nrec - 1], pt[: nrec - 1]) and not back[nrec - 1].any()
 
 
 def test_wire_layout_naive_alltoall():

@@ -27,17 +27,29 @@ def test_ring_matches_oracle(ring_bytes, seed):
     o = oracle.Ring(KEY, iv, ring_bytes)
     rnd = random.Random(seed)
     big = ring_bytes >= (1 << 20)
+    import torch
+
     for step in range(60):
+        before = g.state()
         if rnd.random() < 0.5:
             gen = rnd.choice([1, 16, 100, 1000, 1024, 3000]) if not big else rnd.choice([4096, 1 << 20, 3 << 20])
+            op = ("generate", gen)
             assert g.generate(gen) == o.generate(gen), step
         else:
             n = rnd.choice([0, 1, 15, 16, 17, 100, 999, 2048, 5000]) if not big else rnd.choice([17, 65536, 2 << 20])
+            op = ("encrypt", n)
             pt = splitmix64_bytes(seed * 1000 + step, n)
             out = empty(max(n, 1), fill=0)
-            g.encrypt(out, dev(pt) if n else empty(1), n)
+            inp = dev(pt) if n else empty(1)
+            g.encrypt(out, inp, n)
+        try:  # each step's launches complete before the next: a device fault names its step and op
+            torch.cuda.synchronize()
+        except Exception as e:
+            raise AssertionError(f"device fault at step {step} {op}, ring state before {before}") from e
+        if op[0] == "encrypt":
             want = o.encrypt(pt.tobytes())
             assert host(out)[:n].tobytes() == want, step
+            del inp
         assert g.state() == o.state(), step
 
 

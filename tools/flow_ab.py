@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of two builds of the engine on the FLOW-kernel shapes (config 5's 8 x 1 MiB,
-single 64 KiB messages, 3 x 100000 B, 1 x 8 MiB, 32 x 256 KiB).
+single 64 KiB messages, 3 x 100000 B, 1 x 8 MiB, 32 x 256 KiB) and two ragged ones (8 x (1 MiB - 5),
+65536 x 1000 B on the lane kernel) and short records (1000 B, 100 B; few of them).
 
     python tools/flow_ab.py <libA.so> <libB.so> [rounds]
 
@@ -16,7 +17,10 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHAPES = {"8x1MiB": (1 << 20, 8), "1x64KiB": (65536, 1), "3x100000": (100000, 3), "1x8MiB": (8 << 20, 1),
-          "32x256KiB": (256 << 10, 32)}
+          "32x256KiB": (256 << 10, 32), "8x(1MiB-5)": ((1 << 20) - 5, 8), "65536x1000": (1000, 65536),
+          "1x1000": (1000, 1), "64x1000": (1000, 64), "2048x1000": (1000, 2048), "16x100": (100, 16),
+          "1x100": (100, 1), "2048x600": (600, 2048), "2048x300": (300, 2048), "2048x200": (200, 2048),
+          "256x260": (260, 256), "16x300": (300, 16)}
 
 
 def child() -> None:

@@ -203,10 +203,11 @@ int main(int argc, char** argv) {
     fprintf(stderr, "cmpi_ctx_new: %s\n", cmpi_last_error());
     return 1;
   }
-  const size_t sizes[] = {1024, 4096, 65536};
-  const char* names[] = {"1k", "4k", "64k"};
+  // 1000 and 65000 B: ragged lengths (a partial last block)
+  const size_t sizes[] = {1024, 4096, 65536, 1000, 65000};
+  const char* names[] = {"1k", "4k", "64k", "1000b", "65000b"};
   uint8_t nonce[12] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12};
-  for (int si = 0; si < 3; ++si) {
+  for (int si = 0; si < 5; ++si) {
     const size_t n = sizes[si];
     uint8_t *dp, *dc, *db, *hp, *hc, *hb;
     CK(hipMalloc((void**)&dp, n));
