@@ -18,10 +18,6 @@ struct Svc {
   hipStream_t st = nullptr;
   uint32_t* hw = nullptr;      // page-locked coherent: ring [0..11] (three 16-B chunks), done [32..35]
   uint32_t* dw = nullptr;      // its device address
-  // CMPI_SERVICE_RING=device: the ring in fine-grained device memory, written by the host through
-  // its mapping (the leader polls HBM instead of reading host memory over PCIe); else null
-  uint32_t* dring = nullptr;   // device allocation
-  uint32_t* dring_h = nullptr; // host-writable address of it
   uint32_t* go = nullptr;      // device control words (64 B), counter (at +64), partials (at +128)
   cmpi::dev::u32x4* wts = nullptr;  // device chunk weights (4 x 64 x 4 blocks)
   bool wts_ok = false;
@@ -31,7 +27,7 @@ struct Svc {
   uint32_t gen = 0;            // generation of the last launch
   bool running = false;
   uint32_t idle_us = 2000;
-  uint32_t* ring() { return dring_h ? dring_h : hw; }
+  uint32_t* ring() { return hw; }
   uint32_t* done() { return hw + 32; }
 };
 
@@ -42,13 +38,11 @@ void svc_post(Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc], uint32_t seq) {
   for (uint32_t c = 0; c < 3; ++c)
     for (uint32_t j = 0; j < 3; ++j) r[4 * c + 1 + j] = d[3 * c + j];
   for (uint32_t c = 0; c < 3; ++c) __atomic_store_n(r + 4 * c, seq, __ATOMIC_RELEASE);
-  if (S.dring_h) __builtin_ia32_sfence();  // device mapping may be write-combined: push the words out now
 }
 
 void svc_release(Svc& S) {
   if (S.st) (void)hipStreamDestroy(S.st);
   if (S.hw) (void)hipHostFree(S.hw);
-  if (S.dring) (void)hipFree(S.dring);
   if (S.go) (void)hipFree(S.go);
   if (S.wts) (void)hipFree(S.wts);
   if (S.bounce) (void)hipHostFree(S.bounce);
@@ -78,7 +72,7 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
   if (rc) return rc;
   if ((rc = wait_keys(c, S.st))) return rc;  // tables of a re-key still in flight on the caller's stream
   cmpi::dev::SvcArgs a{};
-  a.ring = S.dring ? S.dring : S.dw;
+  a.ring = S.dw;
   a.done = S.dw + 32;
   a.go = S.go;
   a.cnt = S.go + 16;
@@ -219,19 +213,6 @@ int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
     return fail(CMPI_EHIP, "message service allocation failed");
   }
   memset(S.hw, 0, 256);
-  const char* ring_env = getenv("CMPI_SERVICE_RING");
-  if (ring_env && !strcmp(ring_env, "device")) {  // opt-in experiment: fails loudly if unavailable
-    hipPointerAttribute_t at{};
-    if (hipExtMallocWithFlags((void**)&S.dring, 256, hipDeviceMallocFinegrained) != hipSuccess ||
-        hipMemset(S.dring, 0, 256) != hipSuccess || hipPointerGetAttributes(&at, S.dring) != hipSuccess ||
-        !at.hostPointer) {
-      svc_release(S);
-      delete c->svc;
-      c->svc = nullptr;
-      return fail(CMPI_EHIP, "CMPI_SERVICE_RING=device: no host-writable fine-grained device ring");
-    }
-    S.dring_h = static_cast<uint32_t*>(at.hostPointer);
-  }
   return CMPI_OK;
 }
 
