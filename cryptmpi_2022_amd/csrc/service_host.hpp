@@ -16,7 +16,7 @@ constexpr uint64_t kSvcLifeUs = 100000;           // relaunched at least every 1
 
 struct Svc {
   hipStream_t st = nullptr;
-  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..11] (three 16-B chunks), done [32..35]
+  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..11] (three 16-B chunks), done [32..44]
   uint32_t* dw = nullptr;      // its device address
   uint32_t* go = nullptr;      // device control words (64 B), counter (at +64), partials (at +128)
   cmpi::dev::u32x4* wts = nullptr;  // device chunk weights (4 x 64 x 4 blocks)
@@ -95,7 +95,19 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
 }
 
 // The current generation has exited (idle, lifetime, stop): its exit word is written.
-bool svc_exited(Svc& S) { return __atomic_load_n(S.done() + 2, __ATOMIC_ACQUIRE) == S.gen; }
+bool svc_exited(Svc& S) { return __atomic_load_n(S.done() + 12, __ATOMIC_ACQUIRE) == S.gen; }
+
+// Completion of message `seq`: all five {seq, word} pairs (status, tag words 0-3) carry it; each
+// pair is read as one 8-byte load, so its word belongs to its seq.  w[0] = status, w[1..4] = tag.
+bool svc_done(Svc& S, uint32_t seq, uint32_t (&w)[5]) {
+  const uint64_t* p = reinterpret_cast<const uint64_t*>(S.done());
+  for (int i = 0; i < 5; ++i) {
+    const uint64_t v = __atomic_load_n(p + i, __ATOMIC_ACQUIRE);
+    if ((uint32_t)v != seq) return false;
+    w[i] = (uint32_t)(v >> 32);
+  }
+  return true;
+}
 
 // Stop a running service and drain its stream (ctx free, re-key, cmpi_service_stop).  hmu held.
 int svc_stop_locked(Svc& S) {
@@ -163,12 +175,13 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
   svc_post(S, d, seq);
   const auto t0 = std::chrono::steady_clock::now();
   int relaunches = 0;
+  uint32_t w[5];
   for (uint32_t i = 1;; ++i) {
-    if (__atomic_load_n(S.done(), __ATOMIC_ACQUIRE) == seq) break;
+    if (svc_done(S, seq, w)) break;
     if (svc_exited(S)) {  // the generation ended (lifetime): let every workgroup finish first
       HIP_TRY(hipStreamSynchronize(S.st));
       S.running = false;
-      if (__atomic_load_n(S.done(), __ATOMIC_ACQUIRE) == seq) break;
+      if (svc_done(S, seq, w)) break;
       if (++relaunches > 2) return fail(CMPI_EHIP, "message service did not complete message %u", seq);
       if (int rc = svc_launch(c, S, seq - 1)) return rc;  // it never saw the message
       continue;
@@ -176,12 +189,13 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
     if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
       const hipError_t e = hipStreamQuery(S.st);
       if (e != hipSuccess && e != hipErrorNotReady) return fail(CMPI_EHIP, "service kernel: %s", hipGetErrorString(e));
-      if (e == hipSuccess && __atomic_load_n(S.done(), __ATOMIC_ACQUIRE) != seq && !svc_exited(S))
+      if (e == hipSuccess && !svc_done(S, seq, w) && !svc_exited(S))
         return fail(CMPI_EHIP, "service kernel ended without completing message %u", seq);
     }
   }
-  const int32_t ok = (int32_t)__atomic_load_n(S.done() + 1, __ATOMIC_ACQUIRE);
-  if (hout) memcpy(out, hout, out_rec);
+  const int32_t ok = (int32_t)w[0];
+  if (hout) memcpy(out, hout, len);
+  if (!DEC) memcpy(out + len, w + 1, 16);  // the tag travels in the completion words
   if (DEC) {
     if (status) *status = ok;
     if (ok != 1) return fail(CMPI_EAUTH, "1 of 1 records failed authentication");

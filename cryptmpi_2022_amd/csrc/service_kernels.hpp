@@ -27,9 +27,12 @@
 //           publishes its partial write-through, writes its L2 back to the host (system release)
 //           and adds to an arrival counter — the last arriver XORs the partials
 //           (MI355X_MICROARCH.md, Valid forms: sc1 16-B stores, agent add, sc1 loads by the adder
-//           whose add came last), writes the tag (seal) or checks it (open; zero-fills a forged
-//           message, aead.h:276-278), resets the counter and writes done[1] = status, done[0] =
-//           seq with a system-scope release.
+//           whose add came last), checks the tag (open; zero-fills a forged message,
+//           aead.h:276-278), resets the counter, and after a system-scope release of the record
+//           bytes posts the completion as five 8-byte {seq, word} pairs (status, tag words 0-3) in
+//           three 16-byte system-scope stores: no store waits on another's PCIe acknowledgement,
+//           and the host takes a pair only with the new seq in it, so a pair cannot tear; the host
+//           writes a seal's tag into out + len itself.
 // Every wave's wait loop is bounded by the wall clock: the grid drains even if the host vanishes.
 #pragma once
 #include "gcm_kernels.hpp"
@@ -45,7 +48,7 @@ constexpr uint32_t kSvcDesc = 9u;  // descriptor words: op, len, in lo/hi, out l
 
 struct SvcArgs {
   const uint32_t* ring;  // page-locked host words (device address): chunks [4c] = seq, [4c+1..4c+3] = desc[3c..3c+2]
-  uint32_t* done;        // page-locked host words: [0] completed seq, [1] status, [2] exited generation
+  uint32_t* done;        // page-locked host words: [0..9] five {seq, word} pairs (status, tag 0-3), [12] exited generation
   uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [3] seqlock version, [4..12] descriptor copy
   uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
   u32x4* part;           // device: one partial per workgroup
@@ -65,6 +68,11 @@ __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
 __device__ __forceinline__ u32x4 sys_load16(const uint32_t* p) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p), 0, 16, 0x00020000);
   return __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 17);
+}
+// one 16-byte system-scope write (sc0 sc1) into a page-locked host chunk; p 16-byte aligned
+__device__ __forceinline__ void sys_store16(uint32_t* p, u32x4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, 0, 0, 17);
 }
 __device__ __forceinline__ uint32_t wt_load(const uint32_t* p) {  // write-through word (sc1)
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -166,12 +174,9 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   if (!lds32(kSvcX + 44u)) return;  // workgroup-uniform
   // the last arriver: tag / verdict, then the host word
   if (threadIdx.x == 0u) {
-    const u32x4 tag = lds128(kSvcTag);
     uint32_t ok = 1u;
-    if (!DECRYPT) {
-      st_blk(outp + len, tag);
-    } else {
-      const u32x4 d = ld_blk(inp + len) ^ tag;
+    if (DECRYPT) {
+      const u32x4 d = ld_blk(inp + len) ^ lds128(kSvcTag);
       ok = (d[0] | d[1] | d[2] | d[3]) == 0u ? 1u : 0u;
     }
     lds_st32(kSvcX + 48u, ok);
@@ -186,8 +191,11 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   __syncthreads();
   if (threadIdx.x == 0u) {
     if (ngrp > 1u) wt_store(s.cnt, 0u);
-    __hip_atomic_store(s.done + 1, lds32(kSvcX + 48u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(s.done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the record bytes (every wave waited for its own) reach the host first
+    const u32x4 tag = DECRYPT ? u32x4{0u, 0u, 0u, 0u} : lds128(kSvcTag);
+    sys_store16(s.done, u32x4{seq, lds32(kSvcX + 48u), seq, tag[0]});
+    sys_store16(s.done + 4, u32x4{seq, tag[1], seq, tag[2]});
+    sys_store16(s.done + 8, u32x4{seq, tag[3], 0u, 0u});
   }
 }
 
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
     cur = q;
     t_last = wall_clock64();
   }
-  if (leader && threadIdx.x == 0u) __hip_atomic_store(s.done + 2, s.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (leader && threadIdx.x == 0u) __hip_atomic_store(s.done + 12, s.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace dev
