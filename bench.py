@@ -506,24 +506,36 @@ def host_path_rate(device: int, n: int = 1024, nrec: int = 65536) -> dict:
 A2A_BLOCKS = 8  # BASELINE config 5: 8 ranks, so every rank seals 8 peer blocks of 1 MiB per call
 
 
+def _peer_send(dev, rank: int, nblk: int, n: int):
+    """alltoall_e2e's send buffer of `rank` (seeded per rank: any rank can rebuild a peer's)."""
+    g = torch.Generator(device=dev).manual_seed(4242 + rank)
+    return torch.randint(0, 256, (nblk * n,), dtype=torch.uint8, device=dev, generator=g)
+
+
 def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, warmup: int = 3) -> dict:
     """BASELINE config 5 end to end, MPIR_Naive_Sec_Alltoall (alltoall.c:764-836) per rank:
     seal the rank's 8 peer blocks (config 5's p = 8) with fresh nonces into the wire layout
-    nonce||ct||tag (one batched call), exchange the wire blocks (RCCL all_to_all_single over
-    xGMI; with fewer than 8 ranks each peer gets 8/ranks consecutive blocks, one rank loops them
-    back through a device copy), open the 8 received blocks (one batched call), on one stream.
+    nonce||ct||tag (one batched call), exchange the wire blocks, open the 8 received blocks (one
+    batched call), on one stream.  Transport: RCCL all_to_all_single over xGMI (backend "nccl");
+    with a "gloo" group (ranks sharing one GPU, tests/test_gpu_alltoall8.py) the wire blocks go
+    through page-locked host memory, as a host MPI would carry them; one rank loops them back
+    through a device copy.  With fewer than 8 ranks each peer gets 8/ranks consecutive blocks.
     The per-rank seal/open work is config 5's at every rank count.  Every rank runs this;
-    time = MAX over ranks; rate = plaintext bytes each rank sent / time."""
+    time = MAX over ranks; rate = plaintext bytes each rank sent / time.  After the timed calls
+    every rank checks that it received exactly its peers' plaintext (every block authenticated)."""
     from cryptmpi_2022_amd import _native as N
 
     p = pg.get_world_size() if pg is not None else 1
+    rank = pg.get_rank() if pg is not None else 0
+    host = p > 1 and pg.get_backend() == "gloo"
     nblk = -(-A2A_BLOCKS // p) * p  # a multiple of the rank count (8 for 1, 2, 4, 8 ranks)
     dev = torch.device("cuda", device)
-    g = torch.Generator(device=dev).manual_seed(4242 + (pg.get_rank() if pg is not None else 0))
-    send = torch.randint(0, 256, (nblk * n,), dtype=torch.uint8, device=dev, generator=g)
+    send = _peer_send(dev, rank, nblk, n)
     recv = torch.empty_like(send)
     wire = torch.empty(nblk * (n + 28), dtype=torch.uint8, device=dev)
     wire_in = torch.empty_like(wire)
+    h_out = torch.empty(wire.numel(), dtype=torch.uint8).pin_memory() if host else None
+    h_in = torch.empty_like(h_out).pin_memory() if host else None
     status = torch.zeros(nblk, dtype=torch.int32, device=dev)
     ctx = aead.AeadCtx(KEY, device=device)
     ws_bytes = max(ctx.workspace_size(n, nblk), 16)
@@ -535,7 +547,11 @@ def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, wa
 
     def one():
         N.check(L.cmpi_naive_seal_blocks(ctx.handle, P(wire), P(send), n, nblk, P(ws_seal), st))
-        if pg is not None and p > 1:
+        if host:
+            h_out.copy_(wire)  # synchronous: the seal is done when the host sends
+            pg.all_to_all_single(h_in, h_out)
+            wire_in.copy_(h_in, non_blocking=True)
+        elif p > 1:
             pg.all_to_all_single(wire_in, wire)
         else:
             wire_in.copy_(wire)
@@ -545,8 +561,6 @@ def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, wa
         one()
     torch.cuda.synchronize(dev)
     ok = bool((status == 1).all())
-    if p == 1:
-        ok = ok and torch.equal(recv, send)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -555,27 +569,36 @@ def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, wa
     torch.cuda.synchronize(dev)
     barrier()
     wall = time.perf_counter() - t0
+    # outside the timed region: every block authenticated, and this rank received exactly its
+    # peers' plaintext (chunk `rank` of every peer's send buffer, rebuilt from the peer's seed)
+    ok = ok and bool((status == 1).all())
+    v = nblk // p
+    want = torch.cat([_peer_send(dev, j, nblk, n)[rank * v * n:(rank + 1) * v * n] for j in range(p)])
+    peers_ok = bool(torch.equal(recv, want))
     # parity (outside the timed region): this rank's wire blocks of the last call, nonce||ct||tag,
     # against OpenSSL's seal of the same blocks under the nonces the wire carries
     try:
         wv = wire.view(nblk, n + 28).cpu().numpy()
-        want, bad = OpenSSLRef().aead("gcm", False, wv[:, :12], send.view(nblk, n).cpu().numpy(), n)
-        par = bad == 0 and bool(np.array_equal(wv[:, 12:], want))
+        want_ct, bad = OpenSSLRef().aead("gcm", False, wv[:, :12], send.view(nblk, n).cpu().numpy(), n)
+        par = bad == 0 and bool(np.array_equal(wv[:, 12:], want_ct))
     except Exception:
         par = False
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if pg is not None and p > 1:
+    if p > 1:  # MAX of the wall clocks, MIN of the verdicts (host tensors over gloo)
+        rdev = torch.device("cpu") if host else dev
+        t = torch.tensor([wall], dtype=torch.float64, device=rdev)
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
-        okt = torch.tensor([1 if ok else 0, 1 if par else 0], dtype=torch.int32, device=dev)
+        okt = torch.tensor([int(ok), int(par), int(peers_ok)], dtype=torch.int32, device=rdev)
         pg.all_reduce(okt, op=pg.ReduceOp.MIN)
-        ok, par = bool(okt[0].item()), bool(okt[1].item())
-    wall = float(t.item())
+        wall = float(t.item())
+        ok, par, peers_ok = (bool(x) for x in okt.tolist())
     ctx.close()
+    transport = ("gloo all_to_all_single through page-locked host memory" if host else
+                 "RCCL all_to_all_single (xGMI)" if p > 1 else "1 rank: device copy (blocks looped back)")
     return {"ranks": p, "blocks_per_rank": nblk, "block_bytes": n, "ms_per_call": round(wall / steps * 1e3, 4),
             "GiBps_per_rank": round(nblk * n * steps / wall / GIB, 2),
             "GiBps_all_ranks": round(p * nblk * n * steps / wall / GIB, 2),
-            "transport": "RCCL all_to_all_single (xGMI)" if p > 1 else "1 rank: device copy (blocks looped back)",
-            "all_blocks_authenticated": ok, "parity_cpu": par,
+            "transport": transport, "all_blocks_authenticated": ok, "recv_matches_peers": peers_ok,
+            "parity_cpu": par,
             "parity": "every rank's wire blocks (nonce||ct||tag) vs OpenSSL 3 EVP_aes_128_gcm seal under the wire nonces"}
 
 
@@ -1040,15 +1063,35 @@ def cpu_port_baseline(workload: str, seconds: float = 4.0) -> dict:
 
 
 def load_pmc(workload: str):
-    """HBM traffic per launch of the dominant kernel from a committed rocprofv3 --pmc summary."""
+    """HBM traffic per launch of the dominant kernel from a committed rocprofv3 --pmc summary
+    (profiles/pmc_<workload>.json): (bytes, label naming the file, its round and kernel) or
+    (None, reason).  The counters come from separate --pmc passes of tools/gpu_pmc.sh, not from
+    this run (rocprofv3 cannot collect them inside the bench's timed region)."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(p):
-        return None
+        return None, "no committed PMC summary"
     try:
         with open(p) as f:
-            return json.load(f).get("traffic_bytes_per_launch")
-    except Exception:
-        return None
+            d = json.load(f)
+    except Exception as e:
+        return None, f"unreadable {p}: {e!r}"
+    label = (f"profiles/pmc_{workload}.json ({d.get('round', 'round unrecorded')}, "
+             f"kernel {d.get('dominant_kernel')}, rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+             "separate passes, not this run)")
+    return d.get("traffic_bytes_per_launch"), label
+
+
+def seal_kernel_name(w) -> str:
+    """The seal launch's kernel(s) for this workload, from the plan the library will run
+    (cmpi_debug_gcm_plan for GCM: {L, nseg, G, r0}; L = 64 is the flow decomposition)."""
+    if w.alg == "ocb":
+        return "ocb_batch_kernel<false> + ocb_final_kernel<false>"
+    if w.alg == "ctr":
+        return "ctr_kernel"
+    L, nseg, _, _ = aead.gcm_plan(w.ctx, w.n, w.nrec)
+    if L == 64:
+        return "gcm_flow_kernel<false,...>" + (" + gcm_xor_combine_kernel<false>" if nseg > 1 else "")
+    return f"gcm_lane_kernel<{L}, false>" + (" + gcm_combine_kernel<false>" if nseg > 1 else "")
 
 
 def spawn_ranks(n: int) -> None:
@@ -1151,7 +1194,8 @@ def main() -> None:
     bpl = w.bytes_per_launch()
     kern_ms = seal_ms  # dominant kernel: the seal launch (open is within a few % of it)
     achieved = bpl / (kern_ms * 1e-3) / 1e9
-    traffic = load_pmc(args.workload)
+    traffic, traffic_src = load_pmc(args.workload)
+    kname = seal_kernel_name(w)
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -1174,8 +1218,8 @@ def main() -> None:
         "seal_GiBps_per_gpu": round(per_rank_bytes / (seal_ms * 1e-3) / GIB, 2),
         "open_GiBps_per_gpu": round(per_rank_bytes / (open_ms * 1e-3) / GIB, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "seal launch (gcm_lane_kernel<4,false>)" if w.alg == "gcm" else f"{w.alg} seal launch",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": f"seal launch ({kname})",
                      "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bpl},
         "lds_roofline": lds_roofline(w, kern_ms, local) if w.alg == "gcm" else None,
         "verified_round_trip": ok,

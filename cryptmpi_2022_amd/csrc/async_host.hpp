@@ -68,7 +68,7 @@ int pool_stream(StagePool& P, hipStream_t* st) {
   if (P.streams.empty()) {
     for (size_t i = 0; i < kAsyncStreams; ++i) {
       hipStream_t s;
-      HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      HIP_TRY(lib_stream(&s));
       P.streams.push_back(s);
     }
   }

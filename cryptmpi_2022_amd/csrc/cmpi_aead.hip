@@ -193,6 +193,32 @@ int record_keys(const cmpi_ctx* c, hipStream_t stream) {
   return CMPI_OK;
 }
 
+// The library's own streams (host pipeline, async request pool, message service, staging stream)
+// are made here.  g_stream_mode (test hook cmpi_debug_set_stream_mode) picks the form:
+//   0  hipStreamCreateWithFlags(non-blocking)
+//   1  non-blocking at the greatest priority (its own pool of hardware queues)
+//   2  hipExtStreamCreateWithCUMask over every CU (a hardware queue of its own; blocking)
+std::atomic<int> g_stream_mode{0};
+hipError_t lib_stream(hipStream_t* s) {
+  const int mode = g_stream_mode.load();
+  if (mode == 1) {
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+  }
+  if (mode == 2) {
+    int dev = 0, ncu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    std::vector<uint32_t> m((size_t)(ncu + 31) / 32, ~0u);
+    if (ncu % 32) m.back() = (1u << (ncu % 32)) - 1u;
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)m.size(), m.data());
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 int ensure_buf(void** p, size_t* cap, size_t need) {
   if (need <= *cap) return CMPI_OK;
   if (*p) (void)hipFree(*p);
@@ -910,7 +936,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   std::unique_lock<std::mutex> lk(c->hmu);  // the pipeline and its staging are per ctx
   HostPipe& P = *c->pipe;
   if (!P.init) {
-    for (auto& st : P.s) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    for (auto& st : P.s) HIP_TRY(lib_stream(&st));
     for (int i = 0; i < 2; ++i) {
       HIP_TRY(hipEventCreateWithFlags(&P.in_ready[i], hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&P.k_done[i], hipEventDisableTiming));
@@ -1112,7 +1138,7 @@ template <typename F>
 int host_stream_op(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, unsigned pad, F fn) {
   DeviceGuard dg(c->device);
   std::unique_lock<std::mutex> lk(c->mu);
-  if (!c->hstream) HIP_TRY(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
+  if (!c->hstream) HIP_TRY(lib_stream(&c->hstream));
   const size_t span = ((size_t)pad + n + 15) & ~(size_t)15;
   int rc = ensure_buf((void**)&c->stage, &c->stage_cap, 2 * span);
   if (rc) return rc;
@@ -1305,6 +1331,7 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
 }
 
 void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
+void cmpi_debug_set_stream_mode(int mode) { g_stream_mode.store(mode >= 0 && mode <= 2 ? mode : 0); }
 void cmpi_debug_set_host_spin(int mode) { g_host_spin.store(mode >= 0 && mode <= 3 ? mode : 0); }
 
 void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }

@@ -217,7 +217,7 @@ int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
   Svc& S = *c->svc;
   S.idle_us = idle_us ? std::min<uint32_t>(idle_us, 1000000u) : 2000u;
   if (S.st) return CMPI_OK;
-  if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
+  if (lib_stream(&S.st) != hipSuccess ||
       hipHostMalloc((void**)&S.hw, 256, hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&S.dw, S.hw, 0) != hipSuccess || hipMalloc((void**)&S.go, 256) != hipSuccess ||
       hipMalloc((void**)&S.wts, 4 * 64 * 4 * 16) != hipSuccess || hipMemset(S.go, 0, 256) != hipSuccess) {

@@ -45,6 +45,10 @@ void cmpi_debug_set_host_direct(size_t bytes);
  * 1 spin on a host word written by hipStreamWriteValue32, 2 the same word written by a one-wave
  * kernel, 3 polling hipStreamQuery. */
 void cmpi_debug_set_host_spin(int mode);
+/* How the library creates its own streams from now on (host pipeline, async request pool,
+ * message service): 0 non-blocking (default), 1 non-blocking at the greatest priority,
+ * 2 CU-masked over every CU (a hardware queue of its own). */
+void cmpi_debug_set_stream_mode(int mode);
 /* The plan a GCM batch of nrec x len would use: out = {L, nseg, G, r0}; a wide plan reports
  * L = 64, nseg = chunks per record, G = X-blocks per chunk (64*steps). */
 int cmpi_debug_gcm_plan(const cmpi_ctx *ctx, size_t len, size_t nrec, uint32_t out[4]);

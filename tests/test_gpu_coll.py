@@ -74,7 +74,7 @@ def test_bench_alltoall_e2e_one_rank(n):
     import bench
 
     res = bench.alltoall_e2e(0, None, lambda: None, n=n, steps=2, warmup=1)
-    assert res["ranks"] == 1 and res["all_blocks_authenticated"] and res["ms_per_call"] > 0
+    assert res["ranks"] == 1 and res["all_blocks_authenticated"] and res["recv_matches_peers"] and res["ms_per_call"] > 0
 
 
 def _coll_rank(rank: int, ws: int, port: int, q, n: int = 3000):

@@ -2,8 +2,11 @@
 the per-message EVP_AEAD_CTX_seal / _open of MPI_SEC_Multi_Thread_Send/Recv_OpenMP
 (MV/src/mpi/pt2pt/send.c:294-315, recv.c:322) — served by a kernel that stays resident between
 messages.  Every byte and status against the oracle (oracle/gcm_ref.c: SP 800-38D, pinned to the
-reference's BoringSSL outputs); pinned and pageable buffers; forged tags zero-filled
-with CMPI_EAUTH (aead.h:276-278); idle exit and relaunch; re-key; several contexts at once."""
+published KATs that SURVEY.md §8c records BoringSSL reproducing and to OpenSSL 3 vectors — the
+reference ships no vectors of its own); pinned and pageable buffers; forged tags
+zero-filled with CMPI_EAUTH (aead.h:276-278); idle exit and relaunch; re-key; several contexts at
+once; host buffers whose device address has bit 31 of its low word set (the sign-extension fault
+fixed in service_kernels.hpp lds_ptr64)."""
 import ctypes
 import time
 
@@ -156,3 +159,103 @@ def test_service_refuses_other_contexts():
         sub.service_start(0)
     sub.close()
     master.close()
+
+
+# ---------------------------------------------------------------- high-bit host addresses
+# Round 3's service fault: a descriptor's 64-bit host address travels as two 32-bit words and was
+# rebuilt from a sign-extended readfirstlane of the low word, so an address whose low word has bit
+# 31 set turned into 0xFFFFFFFF'xxxxxxxx (service_kernels.hpp lds_ptr64).  The allocator only
+# sometimes returns such addresses; here the buffers are mapped at fixed ones.
+_MAP_CANDIDATES = [0x7F00_8000_0000, 0x7E00_8000_0000, 0x6F00_8000_0000, 0x5F00_C000_0000, 0x4F00_8000_0000]
+_MAP_BYTES = 4 << 20
+
+
+def _libc():
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    return libc
+
+
+def _dev_ptr(p: int) -> int:
+    hip = ctypes.CDLL("libamdhip64.so")
+    d = ctypes.c_void_p()
+    assert hip.hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(p), 0) == 0
+    return d.value or 0
+
+
+@pytest.fixture
+def high_bit_region():
+    """4 MiB of page-locked host memory mapped at a fixed address whose low 32-bit word has bit 31
+    set (MAP_FIXED_NOREPLACE: never over an existing mapping), registered with cmpi_host_register;
+    its device address is checked to carry that bit too."""
+    libc = _libc()
+    PROT_RW, MAP_PRIV_ANON, MAP_FIXED_NOREPLACE = 0x3, 0x22, 0x100000
+    base = None
+    for a in _MAP_CANDIDATES:
+        r = libc.mmap(ctypes.c_void_p(a), _MAP_BYTES, PROT_RW, MAP_PRIV_ANON | MAP_FIXED_NOREPLACE, -1, 0)
+        if r is not None and r != ctypes.c_void_p(-1).value and r == a:
+            base = a
+            break
+        if r is not None and r != ctypes.c_void_p(-1).value:
+            libc.munmap(ctypes.c_void_p(r), _MAP_BYTES)  # an old kernel ignored the flag: not the address asked
+    assert base is not None, "no fixed high-bit address could be mapped"
+    ctypes.memset(base, 0, _MAP_BYTES)
+    L = N.lib()
+    assert L.cmpi_host_register(ctypes.c_void_p(base), _MAP_BYTES) == N.CMPI_OK
+    hip = ctypes.CDLL("libamdhip64.so")
+    try:
+        d = _dev_ptr(base)
+        assert d & 0x8000_0000 and (d >> 32) not in (0, 0xFFFF_FFFF), hex(d)
+        yield base
+    finally:
+        torch.cuda.synchronize()
+        hip.hipHostUnregister(ctypes.c_void_p(base))
+        libc.munmap(ctypes.c_void_p(base), _MAP_BYTES)
+
+
+@pytest.mark.parametrize("service", [True, False])
+def test_high_bit_host_addresses(high_bit_region, service):
+    """Seal and open from and into host buffers at addresses 0x....8xxx_xxxx (input at the region
+    base, output 2 MiB above it, nonce inside it): through the resident service (one and several
+    workgroups) and through the direct path, every byte and status against the oracle, a forged
+    message zero-filled."""
+    base = high_bit_region
+    half = _MAP_BYTES // 2
+    buf = (ctypes.c_uint8 * _MAP_BYTES).from_address(base)
+    view = np.frombuffer(buf, dtype=np.uint8)
+    src, dst = view[:half], view[half:]
+    ctx = aead.AeadCtx(KEY)
+    if service:
+        ctx.service_start(20000)
+    L = N.lib()
+    nonce_off = half - 64  # the nonce in the region as well (the direct path reads it from there)
+    for n in (1, 1000, 4096, 65536, 300001, 524288):
+        pt = splitmix64_bytes(0xB17 + n, n)
+        nonce = splitmix64_bytes(0x31 + n, 12).tobytes()
+        src[:n] = pt
+        view[nonce_off:nonce_off + 12] = np.frombuffer(nonce, np.uint8)
+        dst[: n + 16] = 0xA5
+        np_ptr = ctypes.c_void_p(base + nonce_off)
+        assert L.cmpi_gcm_seal_host(ctx.handle, ctypes.c_void_p(base + half), n + 16, ctypes.c_void_p(base), n,
+                                    np_ptr, 12, n, 1) == N.CMPI_OK, n
+        want = oracle.gcm_seal(KEY, nonce, pt.tobytes())
+        assert dst[: n + 16].tobytes() == want, n
+        # open: ciphertext at the region base, plaintext into the upper half
+        src[: n + 16] = np.frombuffer(want, np.uint8)
+        dst[:n] = 0x3C
+        st = np.full(1, 7, np.int32)
+        assert L.cmpi_gcm_open_host(ctx.handle, ctypes.c_void_p(base + half), n, ctypes.c_void_p(base), n + 16,
+                                    np_ptr, 12, n, 1, ctypes.c_void_p(st.ctypes.data)) == N.CMPI_OK, n
+        assert st[0] == 1 and dst[:n].tobytes() == pt.tobytes(), n
+        src[n + 3] ^= 0x40  # forged tag
+        dst[:n] = 0x77
+        assert L.cmpi_gcm_open_host(ctx.handle, ctypes.c_void_p(base + half), n, ctypes.c_void_p(base), n + 16,
+                                    np_ptr, 12, n, 1, ctypes.c_void_p(st.ctypes.data)) == N.CMPI_EAUTH, n
+        assert st[0] == 0 and not dst[:n].any(), n
+        if service:
+            assert ctx.service_running(), n
+    if service:
+        ctx.service_stop()
+    ctx.close()

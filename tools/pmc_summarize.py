@@ -23,7 +23,7 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         short = name.split("(")[0].replace("void cmpi::dev::", "")
         agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
         durs[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-out = {"workload": wl, "source": d, "kernels": {}}
+out = {"workload": wl, "source": d, "round": os.environ.get("ROUND", "round unrecorded"), "kernels": {}}
 for k, cs in agg.items():
     avg = {c: sum(v) / len(v) for c, v in cs.items()}
     dur = sum(durs[k]) / len(durs[k])
