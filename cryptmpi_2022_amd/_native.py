@@ -137,6 +137,8 @@ _SIGS = {
     "cmpi_debug_set_host_chunk": ([_S], None),
     "cmpi_debug_gcm_plan": ([_P, _S, _S, _P], _I),
     "cmpi_debug_set_stream_mode": ([_I], None),
+    "cmpi_debug_set_host_slots": ([_I], None),
+    "cmpi_debug_set_span_direct": ([_S], None),
 }
 # only in the diagnostics build (CMPI_LIB=tools/libcmpi_aead_tools.so)
 _TOOLS_SIGS = {

@@ -103,13 +103,14 @@ const std::vector<Blk>& sq_columns() {
 
 }  // namespace
 
-// Host-path pipeline state of a context (aead_host): three streams, two staging slots.
+// Host-path pipeline state of a context (aead_host): three streams, g_host_slots staging slots.
 struct HostPipe {
   hipStream_t s[3] = {nullptr, nullptr, nullptr};  // H2D, kernel, D2H
-  hipEvent_t in_ready[2], k_done[2], slot_free[2];
+  hipEvent_t in_ready[4], k_done[4], slot_free[4];  // per staging slot (g_host_slots <= 4 in use)
   uint8_t* buf = nullptr;   // device staging, 2 slots
   uint8_t* hbuf = nullptr;  // pinned host staging, 2 slots (pageable user buffers)
-  size_t cap = 0;
+  size_t cap = 0;           // bytes per slot
+  size_t ns = 0;            // slots allocated
   int32_t* hst = nullptr;   // pinned per-record open status of the whole batch
   size_t hst_cap = 0;
   uint8_t* dbounce = nullptr;  // pinned: direct path's packed pageable records, nonces, statuses
@@ -198,9 +199,15 @@ int record_keys(const cmpi_ctx* c, hipStream_t stream) {
 //   0  hipStreamCreateWithFlags(non-blocking)
 //   1  non-blocking at the greatest priority (its own pool of hardware queues)
 //   2  hipExtStreamCreateWithCUMask over every CU (a hardware queue of its own; blocking)
+// `own_pool`: the resident message service's stream.  A persistent kernel holds its hardware
+// queue, and streams that HIP maps onto the same queue (at most GPU_MAX_HW_QUEUES = 4 per priority
+// on the test box) wait behind it for up to its lifetime; at the greatest priority it sits in the
+// high-priority pool, away from the caller's and torch's normal-priority streams
+// (tools/queue_probe.py, profiles/r04a_queue_probe.jsonl: a kernel on another stream waited up to
+// 98 ms behind the service at normal priority, <= 0.6 ms once its streams were warm at high).
 std::atomic<int> g_stream_mode{0};
-hipError_t lib_stream(hipStream_t* s) {
-  const int mode = g_stream_mode.load();
+hipError_t lib_stream(hipStream_t* s, bool own_pool = false) {
+  const int mode = own_pool ? 1 : g_stream_mode.load();
   if (mode == 1) {
     int least = 0, greatest = 0;
     hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
@@ -217,6 +224,39 @@ hipError_t lib_stream(hipStream_t* s) {
     return hipExtStreamCreateWithCUMask(s, (uint32_t)m.size(), m.data());
   }
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+// Device memory that held key-derived values (chunk weights H^k, GHASH partials, tables) is
+// zeroed before it is released or reused for another key (powers of H are enough to
+// forge tags under the old key).  Callers have drained the streams that used it.  The memsets run
+// on a library stream of the current device and wipe_sync() waits for them alone (no device-wide
+// synchronise: the per-message 602 path frees contexts at message rate).
+hipStream_t wipe_stream() {
+  static std::mutex m;
+  static std::map<int, hipStream_t> ws;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(m);
+  auto it = ws.find(dev);
+  if (it != ws.end()) return it->second;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  ws[dev] = s;  // process lifetime
+  return s;
+}
+void wipe_dev(void* d, size_t bytes) {
+  if (!d || !bytes) return;
+  hipStream_t s = wipe_stream();
+  if (!s || hipMemsetAsync(d, 0, bytes, s) != hipSuccess) (void)hipMemset(d, 0, bytes);
+}
+void wipe_sync() {
+  if (hipStream_t s = wipe_stream()) (void)hipStreamSynchronize(s);
+}
+void wipe_chw(std::map<std::pair<uint32_t, uint32_t>, void*>& chw) {
+  for (auto& kv : chw) wipe_dev(kv.second, (size_t)kv.first.second * 64);  // nch x 4 weights of 16 B
+  wipe_sync();
+  for (auto& kv : chw) (void)hipFree(kv.second);
+  chw.clear();
 }
 
 int ensure_buf(void** p, size_t* cap, size_t need) {
@@ -745,9 +785,10 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
 // ---------------------------------------------------------------- host staging
 // Host-memory batches (the *_host entry points: CryptMPI's buffers are host memory bound for a
 // NIC).  The batch is cut into chunks of ~g_host_chunk bytes pipelined over
-// three streams with two staging slots:  H2D(i+1) | kernel(i) | D2H(i-1)  overlap, the slot of
-// chunk i is reused by chunk i+2 once D2H(i) completed.  Pinned host buffers (hipHostMalloc /
+// three streams with NS staging slots (3):  H2D(i+1) | kernel(i) | D2H(i-1)  overlap, the slot of
+// chunk i is reused by chunk i+NS once D2H(i) completed.  Pinned host buffers (hipHostMalloc /
 // cmpi_host_register) move by DMA at PCIe rate; pageable ones are staged by the HIP runtime.
+std::atomic<size_t> g_host_slots{3};  // staging slots, 2..4 (cmpi_debug_set_host_slots)
 std::atomic<size_t> g_host_chunk{(size_t)16 << 20};  // 8 / 16 / 32 MiB: 30.1 / 31.2 / 30.6 GiB/s pinned (tools/host_sweep.py)
 
 // true when p lies in page-locked host memory (hipHostMalloc / hipHostRegister): it can be the
@@ -937,7 +978,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   HostPipe& P = *c->pipe;
   if (!P.init) {
     for (auto& st : P.s) HIP_TRY(lib_stream(&st));
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
       HIP_TRY(hipEventCreateWithFlags(&P.in_ready[i], hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&P.k_done[i], hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&P.slot_free[i], hipEventDisableTiming));
@@ -960,6 +1001,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const size_t ip = in_flat ? in_stride : up16(in_rec), op = out_flat ? out_stride : up16(out_rec);
   const bool n_flat = (nrec == 1 || nonce_stride <= 64) && is_pinned(nonces);
   const size_t npitch = n_flat ? nonce_stride : 16;
+  const size_t NS = (size_t)g_host_slots.load();  // staging slots (chunks in flight)
   const size_t per = std::max<size_t>(1, g_host_chunk.load() / std::max<size_t>(std::max(ip, op), 16));
   const size_t K = std::min(per, nrec);  // records per chunk
   // every region and slot 2 MiB aligned (DMA into regions that straddle 2 MiB boundaries ran
@@ -978,19 +1020,20 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const size_t ws_b = up16(std::max(ws_for(K), ws_for(nrec - (nrec - 1) / K * K)));
   const size_t in_b = up2m(ip * K), out_b = up2m(op * K), n_b = up16(npitch * K), st_b = up16(4 * K);
   const size_t slot_b = up2m(in_b + out_b + n_b + st_b + ws_b);
-  if (P.cap < slot_b) {
+  if (P.cap < slot_b || P.ns < NS) {
     for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
     if (P.buf) (void)hipFree(P.buf);
     if (P.hbuf) (void)hipHostFree(P.hbuf);
     P.buf = P.hbuf = nullptr;
     P.cap = 0;
-    if (hipMalloc(&P.buf, 2 * slot_b + ((size_t)2 << 20)) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc staging failed");
-    if (hipHostMalloc(&P.hbuf, 2 * slot_b, hipHostMallocDefault) != hipSuccess) {
+    if (hipMalloc(&P.buf, NS * slot_b + ((size_t)2 << 20)) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc staging failed");
+    if (hipHostMalloc(&P.hbuf, NS * slot_b, hipHostMallocDefault) != hipSuccess) {
       (void)hipFree(P.buf);
       P.buf = nullptr;
       return fail(CMPI_ENOMEM, "hipHostMalloc staging failed");
     }
     P.cap = slot_b;
+    P.ns = NS;
   }
   if (DEC && P.hst_cap < nrec) {  // statuses land here by DMA, chunk by chunk
     for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
@@ -1032,7 +1075,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   };
   // copy chunk ci's outputs from the pinned slot to the user's buffers (after its D2H)
   auto unpack = [&](size_t ci) -> int {
-    const int sl = (int)(ci & 1);
+    const int sl = (int)(ci % NS);
     const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
     HIP_TRY(hipEventSynchronize(P.slot_free[sl]));
     const auto h = layout(sl, P.hbuf);
@@ -1041,17 +1084,17 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   };
   int rc = CMPI_OK;
   for (size_t ci = 0; ci < nchunks && !rc; ++ci) {
-    const int sl = (int)(ci & 1);
+    const int sl = (int)(ci % NS);
     const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
     const auto d = layout(sl, P.buf);
     const auto h = layout(sl, P.hbuf);
     // slot sl was last used by chunk ci-2: its H2D must have read the pinned inputs and its
     // outputs must have been unpacked (done at iteration ci-1) before we overwrite them
-    if (ci >= 2 && cpu_pack) HIP_TRY(hipEventSynchronize(P.in_ready[sl]));
+    if (ci >= NS && cpu_pack) HIP_TRY(hipEventSynchronize(P.in_ready[sl]));
     if (in_rec && !in_pinned) par_copy_records(h.in, ip, in + r0 * in_stride, in_stride, in_rec, nr);
     if (!n_flat)
       for (size_t i = 0; i < nr; ++i) memcpy(h.n + 16 * i, nonces + (r0 + i) * nonce_stride, 12);
-    if (ci >= 2) HIP_TRY(hipStreamWaitEvent(P.s[0], P.slot_free[sl], 0));
+    if (ci >= NS) HIP_TRY(hipStreamWaitEvent(P.s[0], P.slot_free[sl], 0));
     if (in_rec) {
       if (in_flat)
         HIP_TRY(hipMemcpyAsync(d.in, in + r0 * in_stride, (nr - 1) * ip + in_rec, hipMemcpyHostToDevice, P.s[0]));
@@ -1284,15 +1327,18 @@ void cmpi_ctx_free(cmpi_ctx* c) {
     (void)hipEventSynchronize(c->key_ev);
     (void)hipEventDestroy(c->key_ev);
   }
+  wipe_dev(c->scratch, c->scratch_cap);  // segment / chunk partials
+  wipe_dev(c->stage, c->stage_cap);
+  wipe_dev(c->dt, sizeof(DevTables));  // round keys, H, GHASH tables
+  wipe_chw(c->chw);                     // (waits for the memsets above too)
   if (c->scratch) (void)hipFree(c->scratch);
-  for (auto& kv : c->chw) (void)hipFree(kv.second);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
   if (c->pipe) {
     HostPipe& P = *c->pipe;
     if (P.init) {
       for (auto& st : P.s) (void)hipStreamDestroy(st);
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < 4; ++i) {
         (void)hipEventDestroy(P.in_ready[i]);
         (void)hipEventDestroy(P.k_done[i]);
         (void)hipEventDestroy(P.slot_free[i]);
@@ -1306,6 +1352,9 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   }
   if (c->dt) (void)hipFree(c->dt);
   memset(c->key, 0, 16);
+  memset(&c->rk, 0, sizeof c->rk);
+  memset(&c->drk, 0, sizeof c->drk);
+  memset(&c->H, 0, sizeof c->H);
   delete c;
 }
 
@@ -1331,6 +1380,7 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
 }
 
 void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
+void cmpi_debug_set_host_slots(int slots) { g_host_slots.store(slots >= 2 && slots <= 4 ? (size_t)slots : 3); }
 void cmpi_debug_set_stream_mode(int mode) { g_stream_mode.store(mode >= 0 && mode <= 2 ? mode : 0); }
 void cmpi_debug_set_host_spin(int mode) { g_host_spin.store(mode >= 0 && mode <= 3 ? mode : 0); }
 
@@ -1572,8 +1622,7 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   }
   {
     std::lock_guard<std::mutex> lk(dst->mu);
-    for (auto& kv : dst->chw) (void)hipFree(kv.second);
-    dst->chw.clear();
+    wipe_chw(dst->chw);
     dst->mj.clear();
     dst->dev_keys = true;
     memset(dst->key, 0, 16);
@@ -1616,7 +1665,7 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
     std::lock_guard<std::mutex> hl(c->hmu);
     if (c->svc) {  // the service holds the old key and tables: the next message relaunches it
       if (int e = svc_stop_locked(*c->svc)) return e;
-      c->svc->wts_ok = false;
+      svc_wipe(*c->svc);  // its chunk weights (powers of the old H), partials, last message
     }
     if (c->pipe && c->pipe->init)
       for (auto& ps : c->pipe->s) HIP_TRY(hipStreamSynchronize(ps));
@@ -1624,8 +1673,7 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
     if (c->scratch_used) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, c->scratch_ev, 0));
   }
   std::lock_guard<std::mutex> lk(c->mu);
-  for (auto& kv : c->chw) (void)hipFree(kv.second);
-  c->chw.clear();
+  wipe_chw(c->chw);
   c->mj.clear();
   memcpy(c->key, key, 16);
   cmpi::aes128_expand_words(key, c->rk.w);

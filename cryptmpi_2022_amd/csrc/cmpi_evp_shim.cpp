@@ -85,6 +85,9 @@ const long kWindowUs = (long)env_size("CMPI_EVP_COALESCE_US", 30);
 // service (include/cmpi_service.h), which returns its CUs after n us without messages.  0 (default):
 // one kernel launch per EVP call.
 const size_t kServiceUs = env_size("CMPI_EVP_SERVICE_US", 0);
+// idle limit of the drop-in's services: a resident kernel delays device-wide synchronisation
+// (hipDeviceSynchronize) of the whole process until it idles out (cmpi_service.h)
+constexpr size_t kServiceCapUs = 20000;
 
 int pick_device() {
   const char* vars[] = {"CMPI_DEVICE", "MV2_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK",
@@ -137,59 +140,92 @@ bool scrub(Shared* s) {
   return ok;
 }
 
+// A live context with this key is shared; otherwise the oldest idle context is re-keyed on the
+// device (or a new one made) with the pool lock released, and published under the lock — if
+// another thread published the same key meanwhile, that one is shared and ours is destroyed.
 Shared* acquire(const uint8_t* key) {
   Key k;
   memcpy(k.data(), key, 16);
   Pool& P = pool();
-  std::lock_guard<std::mutex> lk(P.m);
-  auto it = P.by_key.find(k);
-  if (it != P.by_key.end()) {  // same key as a live context: share it
-    Shared* s = it->second;
-    ++s->refs;
-    explicit_bzero(k.data(), k.size());
-    return s;
-  }
   Shared* s = nullptr;
-  if (!P.idle.empty()) {  // re-key the oldest idle context on the device
-    s = P.idle.front();
-    P.idle.pop_front();
-    if (cmpi_ctx_rekey(s->c, key, 16, nullptr) != CMPI_OK) {
-      destroy(s);
-      s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(P.m);
+    auto it = P.by_key.find(k);
+    if (it != P.by_key.end()) {  // same key as a live context: share it
+      Shared* live = it->second;
+      ++live->refs;
+      explicit_bzero(k.data(), k.size());
+      return live;
     }
+    if (!P.idle.empty()) {
+      s = P.idle.front();
+      P.idle.pop_front();
+    }
+  }
+  if (s && cmpi_ctx_rekey(s->c, key, 16, nullptr) != CMPI_OK) {
+    destroy(s);
+    s = nullptr;
   }
   if (!s) {
     cmpi_ctx* c = cmpi_ctx_new(CMPI_AES_128_GCM, key, 16, 0, pick_device());
-    if (!c) return nullptr;
+    if (!c) {
+      explicit_bzero(k.data(), k.size());
+      return nullptr;
+    }
     s = new Shared();
     s->c = c;
-    if (kServiceUs && cmpi_service_start(c, (uint32_t)std::min<size_t>(kServiceUs, 1000000)) != CMPI_OK) {
+    if (kServiceUs && cmpi_service_start(c, (uint32_t)std::min<size_t>(kServiceUs, kServiceCapUs)) != CMPI_OK) {
       destroy(s);
+      explicit_bzero(k.data(), k.size());
       return nullptr;
     }
   }
-  s->key = k;
-  s->refs = 1;
-  P.by_key[k] = s;
+  Shared* other = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(P.m);
+    auto it = P.by_key.find(k);
+    if (it != P.by_key.end()) {
+      other = it->second;
+      ++other->refs;
+    } else {
+      s->key = k;
+      s->refs = 1;
+      P.by_key[k] = s;
+    }
+  }
   explicit_bzero(k.data(), k.size());
+  if (other) {
+    destroy(s);
+    return other;
+  }
   return s;
 }
 
+// The last reference: the context leaves by_key under the pool lock, is scrubbed (a device re-key
+// that drains the context's own streams) with the lock released — EVP_AEAD_CTX_new / _free on
+// other OpenMP threads do not wait behind it — and joins the idle list under the lock
+// again.  Contexts beyond the idle cap are destroyed outside the lock as well.
 void release(Shared* s) {
   Pool& P = pool();
-  std::lock_guard<std::mutex> lk(P.m);
-  if (--s->refs > 0) return;
-  P.by_key.erase(s->key);
+  {
+    std::lock_guard<std::mutex> lk(P.m);
+    if (--s->refs > 0) return;
+    P.by_key.erase(s->key);
+  }
   if (kIdleCap == 0 || !scrub(s)) {
     destroy(s);
     return;
   }
-  P.idle.push_back(s);
-  while (P.idle.size() > kIdleCap) {
-    Shared* o = P.idle.front();
-    P.idle.pop_front();
-    destroy(o);
+  std::vector<Shared*> evict;
+  {
+    std::lock_guard<std::mutex> lk(P.m);
+    P.idle.push_back(s);
+    while (P.idle.size() > kIdleCap) {
+      evict.push_back(P.idle.front());
+      P.idle.pop_front();
+    }
   }
+  for (Shared* o : evict) destroy(o);
 }
 
 bool ensure_stage(Shared* s, size_t need) {

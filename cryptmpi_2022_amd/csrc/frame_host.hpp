@@ -69,7 +69,8 @@ std::vector<Seg602> segments_602(const cmpi_602_plan& p, uint32_t first, uint32_
 template <bool DEC>
 int run_602(const cmpi_ctx* c, const cmpi_602_plan& p, const uint8_t header[25], uint8_t* wire_out,
             const uint8_t* wire_in, uint8_t* pt_out, const uint8_t* pt_in, const std::vector<Seg602>& segs,
-            int32_t* status, void* stream, uint64_t pt_base = 0, uint64_t w_base = 0) {
+            int32_t* status, void* stream, uint64_t pt_base = 0, uint64_t w_base = 0, void* ws = nullptr,
+            size_t* ws_need = nullptr) {
   // small message (recv.c:401-440 / send.c:800-803): one segment under the header nonce
   const bool small = p.mode == '1' && p.total <= k602Pipe;
   size_t i = 0;
@@ -106,14 +107,19 @@ int run_602(const cmpi_ctx* c, const cmpi_602_plan& p, const uint8_t header[25],
         ns.flag2_from = (uint32_t)split;
       }
     }
+    if (ws_need) {  // sizing pass: the largest workspace one of the batches needs (they run in turn)
+      *ws_need = std::max(*ws_need, gcm_ws_bytes(c, plan_gcm(c, s0.len, nrec), nrec));
+      i = j;
+      continue;
+    }
     int rc;
     const uint64_t po = s0.pt_off - pt_base, wo = s0.wire_off - w_base;
     if (!DEC) {
       rc = gcm_batch<false>(c, wire_out + wo + 5, w_stride, pt_in + po, pt_stride, small ? nullptr : wire_out + wo,
-                            w_stride, s0.len, nrec, nullptr, nullptr, stream, ns);
+                            w_stride, s0.len, nrec, nullptr, ws, stream, ns);
     } else {
       rc = gcm_batch<true>(c, pt_out + po, pt_stride, wire_in + wo + 5, w_stride, small ? nullptr : wire_in + wo,
-                           w_stride, s0.len, nrec, status ? status + s0.ctr - segs[0].ctr : nullptr, nullptr,
+                           w_stride, s0.len, nrec, status ? status + s0.ctr - segs[0].ctr : nullptr, ws,
                            stream, ns);
     }
     if (rc) return rc;

@@ -38,14 +38,27 @@ struct SpanOut {
   size_t dev_off, len;
 };
 
-// One framed request: device staging of dev_bytes (+ nst statuses), ins copied H2D, launch(D,
-// dstatus, stream) enqueues the device work, outs copied back D2H; statuses land in status[0..nst).
-// order_after: the request first waits for the work enqueued so far on stream `after` (may be the
-// null stream).
+// One framed request: every framed call has one input span (host bytes the device form reads)
+// and one output span (host bytes it writes).  launch(din, dout, dstatus, ws, stream) enqueues the
+// device form with din / dout the device addresses of the two spans and dstatus the segment
+// statuses (open), which land in status[0..nst), ws the request's workspace.  order_after: the request first waits for the
+// work enqueued so far on stream `after` (may be the null stream).
+// Two forms:
+//  * direct (in + out bytes <= g_span_direct): the kernels read and write the caller's
+//    page-locked spans themselves over PCIe (device addresses of the pinned pages); pageable spans
+//    are packed into / unpacked from the request's pinned staging, which the kernels access the
+//    same way.  No DMA command and no device staging: one launch sequence and an event per call,
+//    so the 602 sender's per-outer-message requests cost their launches, not copy submissions.
+//  * DMA (larger calls): the spans are copied H2D into device staging, the device form runs on
+//    it, the output span is copied back D2H (page-locked: straight into the user's pages).
+std::atomic<size_t> g_span_direct{(size_t)16 << 20};
+
+// ws_bytes: device workspace of the request's own (the 602 batches' partials): requests of one
+// context then run concurrently on their pooled streams instead of queueing on the context's
+// scratch lease one after the other.
 template <class Launch>
-int span_begin(const cmpi_ctx* c, size_t dev_bytes, const std::vector<SpanIn>& ins, const std::vector<SpanOut>& outs,
-               int32_t* status, size_t nst, bool dec, bool order_after, hipStream_t after, Launch launch,
-               cmpi_req** req) {
+int span_begin(const cmpi_ctx* c, size_t dev_bytes, const SpanIn& in, const SpanOut& out, int32_t* status, size_t nst,
+               bool dec, bool order_after, hipStream_t after, Launch launch, cmpi_req** req, size_t ws_bytes = 0) {
   if (!req) return fail(CMPI_EINVAL, "null request");
   *req = nullptr;
   if (!c) return fail(CMPI_EINVAL, "null ctx");
@@ -61,6 +74,13 @@ int span_begin(const cmpi_ctx* c, size_t dev_bytes, const std::vector<SpanIn>& i
     req_release(r);
     return rc;
   };
+  // every HIP failure after the request exists goes through bail (the request, its
+  // pooled stream's work and its staging are released, not leaked)
+#define SPAN_TRY(expr)                                                                        \
+  do {                                                                                        \
+    const hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return bail(fail(CMPI_EHIP, "%s: %s", #expr, hipGetErrorString(e_))); \
+  } while (0)
   int rc = pool_stream(P, &r->st);
   if (rc) return bail(rc);
   {
@@ -82,42 +102,44 @@ int span_begin(const cmpi_ctx* c, size_t dev_bytes, const std::vector<SpanIn>& i
     if (!ok) return bail(fail(CMPI_EHIP, "ordering after the caller's stream failed"));
   }
   auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  const size_t d_st = up16(dev_bytes), d_total = d_st + up16(4 * nst) + 16;
-  if ((rc = pool_take(P, false, d_total, &r->dbuf, &r->dcap))) return bail(rc);
-  uint8_t* D = (uint8_t*)r->dbuf;
-  // pinned staging: pageable inputs, pageable outputs, statuses
-  size_t h_total = 0;
-  std::vector<size_t> in_at(ins.size(), SIZE_MAX), out_at(outs.size(), SIZE_MAX);
-  for (size_t i = 0; i < ins.size(); ++i)
-    if (ins[i].len && !is_pinned(ins[i].host)) in_at[i] = h_total, h_total += up16(ins[i].len);
-  for (size_t i = 0; i < outs.size(); ++i)
-    if (outs[i].len && !is_pinned(outs[i].host)) out_at[i] = h_total, h_total += up16(outs[i].len);
-  const size_t h_st = h_total;
-  h_total += up16(4 * nst) + 16;
+  const bool direct = in.len + out.len <= g_span_direct.load();
+  const uint8_t* in_pin = in.len && direct ? (const uint8_t*)pinned_dev_ptr(in.host) : nullptr;
+  uint8_t* out_pin = out.len && direct ? (uint8_t*)pinned_dev_ptr(out.host) : nullptr;
+  const bool in_pg = in.len && (direct ? !in_pin : !is_pinned(in.host));
+  const bool out_pg = out.len && (direct ? !out_pin : !is_pinned(out.host));
+  // pinned staging: pageable input, pageable output, statuses
+  const size_t h_in = 0, h_out = in_pg ? up16(in.len) : 0, h_st = h_out + (out_pg ? up16(out.len) : 0);
+  const size_t h_total = h_st + up16(4 * nst) + 16;
   if ((rc = pool_take(P, true, h_total, &r->hbuf, &r->hcap))) return bail(rc);
   uint8_t* H = (uint8_t*)r->hbuf;
-  for (size_t i = 0; i < ins.size(); ++i) {
-    if (!ins[i].len) continue;
-    const uint8_t* src = ins[i].host;
-    if (in_at[i] != SIZE_MAX) {
-      par_copy_span(H + in_at[i], src, ins[i].len);
-      src = H + in_at[i];
-    }
-    HIP_TRY(hipMemcpyAsync(D + ins[i].dev_off, src, ins[i].len, hipMemcpyHostToDevice, st));
+  if (in_pg) par_copy_span(H + h_in, in.host, in.len);
+  if (out_pg) {
+    r->span_dst.emplace_back(out.host, H + h_out);
+    r->span_len.push_back(out.len);
   }
-  if ((rc = launch(D, dec ? (int32_t*)(D + d_st) : nullptr, st))) return bail(rc);
-  for (size_t i = 0; i < outs.size(); ++i) {
-    if (!outs[i].len) continue;
-    uint8_t* dst = out_at[i] != SIZE_MAX ? H + out_at[i] : outs[i].host;
-    HIP_TRY(hipMemcpyAsync(dst, D + outs[i].dev_off, outs[i].len, hipMemcpyDeviceToHost, st));
-    if (out_at[i] != SIZE_MAX) {
-      r->span_dst.emplace_back(outs[i].host, H + out_at[i]);
-      r->span_len.push_back(outs[i].len);
-    }
-  }
-  if (dec && nst) HIP_TRY(hipMemcpyAsync(H + h_st, D + d_st, 4 * nst, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipEventRecord(r->done, st));
   r->h_status = (int32_t*)(H + h_st);
+  if (direct) {
+    uint8_t* dH = (uint8_t*)pinned_dev_ptr(H);
+    if (!dH) return bail(fail(CMPI_EHIP, "staging buffer has no device address"));
+    if (ws_bytes && (rc = pool_take(P, false, ws_bytes, &r->dbuf, &r->dcap))) return bail(rc);
+    // an empty span still gets a valid device address (never accessed), as in the DMA form
+    const uint8_t* din = !in.len || in_pg ? dH + h_in : in_pin;
+    uint8_t* dout = !out.len || out_pg ? dH + h_out : out_pin;
+    if ((rc = launch(din, dout, dec ? (int32_t*)(dH + h_st) : nullptr, ws_bytes ? r->dbuf : nullptr, st)))
+      return bail(rc);
+  } else {
+    const size_t d_st = up16(dev_bytes), d_ws = (d_st + 4 * nst + 255) & ~(size_t)255, d_total = d_ws + ws_bytes + 16;
+    if ((rc = pool_take(P, false, d_total, &r->dbuf, &r->dcap))) return bail(rc);
+    uint8_t* D = (uint8_t*)r->dbuf;
+    if (in.len) SPAN_TRY(hipMemcpyAsync(D + in.dev_off, in_pg ? H + h_in : in.host, in.len, hipMemcpyHostToDevice, st));
+    if ((rc = launch(D + in.dev_off, D + out.dev_off, dec ? (int32_t*)(D + d_st) : nullptr, ws_bytes ? D + d_ws : nullptr,
+                     st)))
+      return bail(rc);
+    if (out.len) SPAN_TRY(hipMemcpyAsync(out_pg ? H + h_out : out.host, D + out.dev_off, out.len, hipMemcpyDeviceToHost, st));
+    if (dec && nst) SPAN_TRY(hipMemcpyAsync(H + h_st, D + d_st, 4 * nst, hipMemcpyDeviceToHost, st));
+  }
+  SPAN_TRY(hipEventRecord(r->done, st));
+#undef SPAN_TRY
   *req = r;
   return CMPI_OK;
 }
@@ -141,6 +163,8 @@ int spans_602(const cmpi_602_plan& p, uint32_t first, uint32_t count, Spans602& 
 
 int sync_req(int rc, cmpi_req* r) { return rc ? rc : cmpi_wait(r); }
 
+constexpr uint32_t k602HostGroup = 4;  // outer messages per request of the synchronous 602 host calls
+
 }  // namespace
 
 extern "C" {
@@ -157,24 +181,34 @@ int cmpi_602_seal_host_begin(const cmpi_ctx* c, const cmpi_602_plan* plan, const
   const cmpi_602_plan p = *plan;
   uint8_t hdr[25];
   memcpy(hdr, header, 25);
-  auto launch = [&](uint8_t* D, int32_t*, hipStream_t st) -> int {
-    if (s.segs.empty()) return CMPI_OK;
-    return run_602<false>(c, p, hdr, D + d_w, nullptr, nullptr, D + d_pt, s.segs, nullptr, st, s.pt_off, s.w_off);
-  };
   // a small message (one segment under the header nonce) has no prefix on the wire: its 5 bytes are
-  // not written (as by cmpi_602_seal), so they are not copied back either
+  // not written (as by cmpi_602_seal), so they are not part of the output span either
   const size_t skip = p.mode == '1' && p.total <= k602Pipe ? 5 : 0;
-  return span_begin(c, d_w + s.w_len, {{in ? in + s.pt_off : nullptr, d_pt, s.pt_len}},
-                    {{wire + s.w_off + skip, d_w + skip, s.w_len - skip}}, nullptr, 0, false, false, nullptr, launch, req);
+  auto launch = [&](const uint8_t* din, uint8_t* dout, int32_t*, void* ws, hipStream_t st) -> int {
+    if (s.segs.empty()) return CMPI_OK;
+    return run_602<false>(c, p, hdr, dout - skip, nullptr, nullptr, din, s.segs, nullptr, st, s.pt_off, s.w_off, ws);
+  };
+  size_t ws = 0;
+  if (!s.segs.empty() &&
+      (rc = run_602<false>(c, p, hdr, nullptr, nullptr, nullptr, nullptr, s.segs, nullptr, nullptr, 0, 0, nullptr, &ws)))
+    return rc;
+  return span_begin(c, d_w + s.w_len, {in ? in + s.pt_off : nullptr, d_pt, s.pt_len},
+                    {wire + s.w_off + skip, d_w + skip, s.w_len - skip}, nullptr, 0, false, false, nullptr, launch, req,
+                    ws);
 }
 
 int cmpi_602_seal_host(const cmpi_ctx* c, const cmpi_602_plan* plan, const uint8_t header[25], uint8_t* wire,
                        const uint8_t* in) {
   int rc = check_602(plan);
   if (rc) return rc;
-  // one request per outer message, all enqueued before the first wait: the pipeline of send.c:754-835
-  std::vector<cmpi_req*> reqs(plan->outer, nullptr);
-  for (uint32_t o = 0; o < plan->outer && !rc; ++o) rc = cmpi_602_seal_host_begin(c, plan, header, wire, in, o, 1, &reqs[o]);
+  // requests of k602HostGroup outer messages, all enqueued before the first wait: the pipeline of
+  // send.c:754-835 with fewer, larger requests (the caller of the whole message has no MPI_Isend
+  // to post between outer messages)
+  std::vector<cmpi_req*> reqs;
+  for (uint32_t o = 0; o < plan->outer && !rc; o += k602HostGroup) {
+    reqs.push_back(nullptr);
+    rc = cmpi_602_seal_host_begin(c, plan, header, wire, in, o, std::min(k602HostGroup, plan->outer - o), &reqs.back());
+  }
   const int w = cmpi_waitall(reqs.data(), reqs.size());
   return rc ? rc : w;
 }
@@ -190,13 +224,17 @@ int cmpi_602_open_host_begin(const cmpi_ctx* c, const uint8_t header[25], uint8_
   const size_t d_w = 0, d_pt = (s.w_len + 255) & ~(size_t)255;
   uint8_t hdr[25];
   memcpy(hdr, header, 25);
-  auto launch = [&](uint8_t* D, int32_t* dst, hipStream_t st) -> int {
+  auto launch = [&](const uint8_t* din, uint8_t* dout, int32_t* dst, void* ws, hipStream_t st) -> int {
     if (s.segs.empty()) return CMPI_OK;
-    return run_602<true>(c, p, hdr, nullptr, D + d_w, D + d_pt, nullptr, s.segs, dst, st, s.pt_off, s.w_off);
+    return run_602<true>(c, p, hdr, nullptr, din, dout, nullptr, s.segs, dst, st, s.pt_off, s.w_off, ws);
   };
+  size_t ws = 0;
+  if (!s.segs.empty() &&
+      (rc = run_602<true>(c, p, hdr, nullptr, nullptr, nullptr, nullptr, s.segs, nullptr, nullptr, 0, 0, nullptr, &ws)))
+    return rc;
   const size_t first_seg = s.segs.empty() ? 0 : s.segs.front().ctr;
-  return span_begin(c, d_pt + s.pt_len, {{wire + s.w_off, d_w, s.w_len}}, {{out + s.pt_off, d_pt, s.pt_len}},
-                    status ? status + first_seg : nullptr, s.segs.size(), true, false, nullptr, launch, req);
+  return span_begin(c, d_pt + s.pt_len, {wire + s.w_off, d_w, s.w_len}, {out + s.pt_off, d_pt, s.pt_len},
+                    status ? status + first_seg : nullptr, s.segs.size(), true, false, nullptr, launch, req, ws);
 }
 
 int cmpi_602_open_host(const cmpi_ctx* c, const uint8_t header[25], uint8_t* out, const uint8_t* wire,
@@ -204,8 +242,11 @@ int cmpi_602_open_host(const cmpi_ctx* c, const uint8_t header[25], uint8_t* out
   cmpi_602_plan p;
   int rc = cmpi_602_plan_from_header(header, &p);
   if (rc) return rc;
-  std::vector<cmpi_req*> reqs(p.outer, nullptr);
-  for (uint32_t o = 0; o < p.outer && !rc; ++o) rc = cmpi_602_open_host_begin(c, header, out, wire, o, 1, status, &reqs[o]);
+  std::vector<cmpi_req*> reqs;
+  for (uint32_t o = 0; o < p.outer && !rc; o += k602HostGroup) {
+    reqs.push_back(nullptr);
+    rc = cmpi_602_open_host_begin(c, header, out, wire, o, std::min(k602HostGroup, p.outer - o), status, &reqs.back());
+  }
   const int w = cmpi_waitall(reqs.data(), reqs.size());
   return rc ? rc : w;
 }
@@ -216,10 +257,10 @@ int cmpi_700_send_host_begin(const cmpi_ctx* c, const uint8_t send_iv[16], uint6
   if (!c || !send_iv || !counter || !header) return fail(CMPI_EINVAL, "null argument");
   if (n && (!in || !out)) return fail(CMPI_EINVAL, "null buffer");
   const size_t d_out = (n + 255) & ~(size_t)255;
-  auto launch = [&](uint8_t* D, int32_t*, hipStream_t st) -> int {
-    return cmpi_700_send(c, send_iv, counter, n ? D : nullptr, n, header, n ? D + d_out : nullptr, st);
+  auto launch = [&](const uint8_t* din, uint8_t* dout, int32_t*, void*, hipStream_t st) -> int {
+    return cmpi_700_send(c, send_iv, counter, din, n, header, dout, st);
   };
-  return span_begin(c, d_out + n, {{in, 0, n}}, {{out, d_out, n}}, nullptr, 0, false, false, nullptr, launch, req);
+  return span_begin(c, d_out + n, {in, 0, n}, {out, d_out, n}, nullptr, 0, false, false, nullptr, launch, req);
 }
 
 int cmpi_700_send_host(const cmpi_ctx* c, const uint8_t send_iv[16], uint64_t* counter, const uint8_t* in, size_t n,
@@ -235,10 +276,10 @@ int cmpi_700_recv_host_begin(const cmpi_ctx* c, const uint8_t recv_iv[16], const
   if (n > out_cap) return fail(CMPI_EINVAL, "header announces %zu bytes, out holds %zu", n, out_cap);
   if (n && (!in || !out)) return fail(CMPI_EINVAL, "null buffer");
   const size_t d_out = (n + 255) & ~(size_t)255;
-  auto launch = [&](uint8_t* D, int32_t*, hipStream_t st) -> int {
-    return cmpi_700_recv(c, recv_iv, header, n ? D + d_out : nullptr, n, n ? D : nullptr, st);
+  auto launch = [&](const uint8_t* din, uint8_t* dout, int32_t*, void*, hipStream_t st) -> int {
+    return cmpi_700_recv(c, recv_iv, header, dout, n, din, st);
   };
-  return span_begin(c, d_out + n, {{in, 0, n}}, {{out, d_out, n}}, nullptr, 0, false, false, nullptr, launch, req);
+  return span_begin(c, d_out + n, {in, 0, n}, {out, d_out, n}, nullptr, 0, false, false, nullptr, launch, req);
 }
 
 int cmpi_700_recv_host(const cmpi_ctx* c, const uint8_t recv_iv[16], const uint8_t header[26], uint8_t* out,
@@ -254,11 +295,11 @@ int cmpi_702_send_host_begin(cmpi_702_sender* s, int pending_isends, const uint8
   if (n && (!in || !out)) return fail(CMPI_EINVAL, "null buffer");
   const size_t d_out = (n + 255) & ~(size_t)255;
   int segs = 0;
-  auto launch = [&](uint8_t* D, int32_t*, hipStream_t st) -> int {
-    segs = cmpi_702_send(s, pending_isends, n ? D : nullptr, n, header, n ? D + d_out : nullptr, st);
+  auto launch = [&](const uint8_t* din, uint8_t* dout, int32_t*, void*, hipStream_t st) -> int {
+    segs = cmpi_702_send(s, pending_isends, din, n, header, dout, st);
     return segs < 0 ? segs : CMPI_OK;
   };
-  const int rc = span_begin(s->ctx, d_out + n, {{in, 0, n}}, {{out, d_out, n}}, nullptr, 0, false, false, nullptr, launch, req);
+  const int rc = span_begin(s->ctx, d_out + n, {in, 0, n}, {out, d_out, n}, nullptr, 0, false, false, nullptr, launch, req);
   if (!rc && segments) *segments = segs;
   return rc;
 }
@@ -280,11 +321,11 @@ int cmpi_702_recv_host_begin(const cmpi_ctx* c, const uint8_t recv_iv[32], const
   if (n > out_cap) return fail(CMPI_EINVAL, "header announces %zu bytes, out holds %zu", n, out_cap);
   if (n && (!in || !out)) return fail(CMPI_EINVAL, "null buffer");
   const size_t d_out = (n + 255) & ~(size_t)255;
-  auto launch = [&](uint8_t* D, int32_t*, hipStream_t st) -> int {
-    return cmpi_702_recv(c, recv_iv, header, n ? D + d_out : nullptr, n, n ? D : nullptr, mask, mask_len, st);
+  auto launch = [&](const uint8_t* din, uint8_t* dout, int32_t*, void*, hipStream_t st) -> int {
+    return cmpi_702_recv(c, recv_iv, header, dout, n, din, mask, mask_len, st);
   };
   // the mask (device) was made on mask_stream while the payload was in flight: order after it
-  return span_begin(c, d_out + n, {{in, 0, n}}, {{out, d_out, n}}, nullptr, 0, false, mask != nullptr,
+  return span_begin(c, d_out + n, {in, 0, n}, {out, d_out, n}, nullptr, 0, false, mask != nullptr,
                     (hipStream_t)mask_stream, launch, req);
 }
 
@@ -293,5 +334,7 @@ int cmpi_702_recv_host(const cmpi_ctx* c, const uint8_t recv_iv[32], const uint8
   cmpi_req* r = nullptr;
   return sync_req(cmpi_702_recv_host_begin(c, recv_iv, header, out, out_cap, in, mask, mask_len, mask_stream, &r), r);
 }
+
+void cmpi_debug_set_span_direct(size_t bytes) { g_span_direct.store(bytes); }
 
 }  // extern "C"

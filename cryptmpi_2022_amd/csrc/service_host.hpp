@@ -40,7 +40,21 @@ void svc_post(Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc], uint32_t seq) {
   for (uint32_t c = 0; c < 3; ++c) __atomic_store_n(r + 4 * c, seq, __ATOMIC_RELEASE);
 }
 
+constexpr size_t kSvcWtsBytes = 4 * 64 * 4 * 16;
+
+// Key-derived and message bytes the service keeps between messages: the chunk weights (powers of
+// H), the workgroup partials, the bounce buffer's last message.  Stream drained.
+void svc_wipe(Svc& S) {
+  wipe_dev(S.wts, kSvcWtsBytes);
+  wipe_dev(S.go, 256);
+  if (S.bounce) memset(S.bounce, 0, S.bcap);
+  S.wts_ok = false;
+  wipe_sync();  // svc_weights' next upload must land after the wipe
+}
+
 void svc_release(Svc& S) {
+  svc_wipe(S);
+  wipe_sync();  // the memsets before the frees
   if (S.st) (void)hipStreamDestroy(S.st);
   if (S.hw) (void)hipHostFree(S.hw);
   if (S.go) (void)hipFree(S.go);
@@ -217,10 +231,10 @@ int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
   Svc& S = *c->svc;
   S.idle_us = idle_us ? std::min<uint32_t>(idle_us, 1000000u) : 2000u;
   if (S.st) return CMPI_OK;
-  if (lib_stream(&S.st) != hipSuccess ||
+  if (lib_stream(&S.st, true) != hipSuccess ||
       hipHostMalloc((void**)&S.hw, 256, hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&S.dw, S.hw, 0) != hipSuccess || hipMalloc((void**)&S.go, 256) != hipSuccess ||
-      hipMalloc((void**)&S.wts, 4 * 64 * 4 * 16) != hipSuccess || hipMemset(S.go, 0, 256) != hipSuccess) {
+      hipMalloc((void**)&S.wts, kSvcWtsBytes) != hipSuccess || hipMemset(S.go, 0, 256) != hipSuccess) {
     svc_release(S);
     delete c->svc;
     c->svc = nullptr;

@@ -21,6 +21,8 @@ extern "C" {
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments);
 /* Chunk bytes of the pipelined host path (*_host calls; 0 = default 16 MiB). */
 void cmpi_debug_set_host_chunk(size_t bytes);
+/* Staging slots (chunks in flight) of the pipelined host path: 2..4, anything else = default 3. */
+void cmpi_debug_set_host_slots(int slots);
 /* Wide GCM decomposition (gcm_flow_kernel: one wavefront per 64*steps-block chunk of a record,
  * for few long records): mode 0 automatic, 1 always when legal (>= 64 data blocks), -1 never;
  * steps per chunk (0 = automatic; rounded down to a power of two on device-keyed contexts). */
@@ -45,6 +47,10 @@ void cmpi_debug_set_host_direct(size_t bytes);
  * 1 spin on a host word written by hipStreamWriteValue32, 2 the same word written by a one-wave
  * kernel, 3 polling hipStreamQuery. */
 void cmpi_debug_set_host_spin(int mode);
+/* Framed host-memory requests (602 / 700 / 702 *_host calls) whose input + output spans total at
+ * most `bytes` run direct: the kernels access the page-locked spans over PCIe, no DMA copies
+ * (default 16 MiB; 0 = always DMA). */
+void cmpi_debug_set_span_direct(size_t bytes);
 /* How the library creates its own streams from now on (host pipeline, async request pool,
  * message service): 0 non-blocking (default), 1 non-blocking at the greatest priority,
  * 2 CU-masked over every CU (a hardware queue of its own). */

@@ -13,7 +13,14 @@
  *
  * The kernel returns its CUs after `idle_us` microseconds without a message (0 = 2000) and at
  * least every 100 ms; the next message relaunches it.  While it runs it occupies 8 CUs: large
- * batches launched meanwhile on other streams share the remaining CUs.
+ * batches launched meanwhile on other streams share the remaining CUs.  The kernel also holds
+ * the hardware queue of its stream, which the library creates at the greatest stream priority:
+ * HIP maps streams of one priority onto at most GPU_MAX_HW_QUEUES hardware queues, and work on a
+ * stream that shares the service's queue waits until the kernel exits (idle_us, at most 100 ms).
+ * Normal-priority streams (the caller's, torch's, the library's other streams) never share it;
+ * other greatest-priority streams of the process and more than GPU_MAX_HW_QUEUES concurrently
+ * running services may.  hipDeviceSynchronize / torch.cuda.synchronize() wait for the kernel to
+ * exit: call cmpi_service_stop first, or keep idle_us short.
  * Host-keyed AES-128-GCM contexts only (CMPI_EINVAL otherwise).  cmpi_ctx_rekey and
  * cmpi_ctx_rekey_subkey stop a running service (the next message restarts it with the new key;
  * a device-keyed context ends the service).  cmpi_ctx_free stops it.

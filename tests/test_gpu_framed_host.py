@@ -2,7 +2,9 @@
 sender / receiver (MV/src/mpi/pt2pt/send.c:729-850, recv.c:679-809) with one request per outer
 512 KiB message, begun and completed in order; the 700 / 702 counter-mode messages straight from
 MPI user buffers (send.c:886-1017, :1502-1987; recv.c:812-940, :1025-1403).  Bytes bit-exact vs the
-oracle's restatement (oracle/framing_ref.c, oracle/ctrmode_ref.c), pageable and page-locked."""
+oracle's restatement (oracle/framing_ref.c, oracle/ctrmode_ref.c), pageable and page-locked, in
+both request forms: direct (the kernels access the page-locked spans over PCIe, the default up to
+16 MiB per request) and DMA (spans copied through device staging)."""
 import numpy as np
 import pytest
 import torch
@@ -19,6 +21,14 @@ pytestmark = pytest.mark.gpu
 KEY = bytes(range(16))
 SMALL_KEY = bytes(16)
 IV32 = splitmix64_bytes(0x702, 32).tobytes()
+
+
+@pytest.fixture(autouse=True, params=["direct", "dma"])
+def span_mode(request):
+    """Every test in both request forms (cmpi_debug_set_span_direct: 16 MiB default / 0)."""
+    N.lib().cmpi_debug_set_span_direct(16 << 20 if request.param == "direct" else 0)
+    yield request.param
+    N.lib().cmpi_debug_set_span_direct(16 << 20)
 
 
 def _buf(n: int, pinned: bool, fill: int = 0):

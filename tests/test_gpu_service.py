@@ -148,6 +148,35 @@ def test_service_two_contexts():
     b.close()
 
 
+def test_service_leaves_other_streams_free():
+    """While the service kernel is resident, kernels on 8 other (normal-priority) streams and on the
+    default stream complete without waiting for it: the service's stream sits in the greatest-
+    priority queue pool (at normal priority one of them shared its hardware queue and
+    waited up to the kernel's 100 ms lifetime, profiles/r04a_queue_probe.jsonl)."""
+    streams = [torch.cuda.Stream() for _ in range(8)]
+    x = torch.ones(16, device="cuda")
+    for s in streams:  # first use of each stream (queue creation, code object load) before timing
+        with torch.cuda.stream(s):
+            x.add_(1)
+        s.synchronize()
+    ctx = aead.AeadCtx(KEY)
+    ctx.service_start(500000)  # 0.5 s idle: resident through the whole check
+    pt = splitmix64_bytes(77, 4096).tobytes()
+    assert ctx.seal(bytes(12), pt) == oracle.gcm_seal(KEY, bytes(12), pt)
+    assert ctx.service_running()
+    lat = []
+    for s in streams + [torch.cuda.current_stream()]:
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s):
+            x.add_(1)
+        s.synchronize()
+        lat.append(time.perf_counter() - t0)
+    assert ctx.service_running()  # still resident: nothing above waited for it to exit
+    ctx.service_stop()
+    ctx.close()
+    assert max(lat) < 0.02, [round(v * 1e3, 2) for v in lat]
+
+
 def test_service_refuses_other_contexts():
     ocb = aead.AeadCtx(KEY, "aes-128-ocb")
     with pytest.raises(N.CmpiError):

@@ -16,6 +16,7 @@
 
 #include "../include/cmpi_aead.h"
 #include "../include/cmpi_debug.h"
+#include "../include/cmpi_ctrmode.h"
 #include "../include/cmpi_service.h"
 
 #define CK(x)                                                                            \
@@ -288,6 +289,73 @@ int main(int argc, char** argv) {
     CK(hipHostFree(hb));
   }
   cmpi_ctx_free(c);
+  {  // 702 messages (send.c:1537-1731, recv.c:1107-1220), device-resident, 4 KiB and 1 KiB:
+     // stream A from the mask ring (the sender's precompute refills it), receiver premask + XOR
+    uint8_t key2[16];
+    for (int i = 0; i < 16; ++i) key2[i] = (uint8_t)(i + 100);
+    cmpi_ctx* cc = cmpi_ctx_new(CMPI_AES_128_CTR, key2, 16, 0, 0);
+    if (!cc) {
+      fprintf(stderr, "cmpi_ctx_new ctr: %s\n", cmpi_last_error());
+      return 1;
+    }
+    uint8_t iv[32];
+    for (int i = 0; i < 32; ++i) iv[i] = (uint8_t)(3 * i + 1);
+    cmpi_702_sender* snd = cmpi_702_sender_new(cc, iv, (size_t)8 << 20, 8, s);
+    if (!snd) {
+      fprintf(stderr, "cmpi_702_sender_new: %s\n", cmpi_last_error());
+      return 1;
+    }
+    for (size_t n : {(size_t)4096, (size_t)1024}) {
+      uint8_t *dpt, *dct, *dbk, *dmask;
+      CK(hipMalloc((void**)&dpt, n));
+      CK(hipMalloc((void**)&dct, n));
+      CK(hipMalloc((void**)&dbk, n));
+      CK(hipMalloc((void**)&dmask, n + 1024));
+      CK(hipMemset(dpt, 0x5a, n));
+      uint8_t hdr[26];
+      size_t ml = 0;
+      auto msg = [&](bool precompute) {
+        if (cmpi_702_send(snd, 0, dpt, n, hdr, dct, s) < 1) CM(-1);
+        if (precompute) CM(cmpi_702_precompute(snd, n, 2, s) < 0);
+        CM(cmpi_702_recv_premask(cc, iv, hdr, dmask, n + 1024, &ml, s));
+        CM(cmpi_702_recv(cc, iv, hdr, dbk, n, dct, dmask, ml, s));
+      };
+      char k[96];
+      const char* nm = n == 4096 ? "4k" : "1k";
+      snprintf(k, sizeof k, "c702_%s_send_precompute_recv_spin_us", nm);
+      put(k, median_us(iters, [&] {
+            msg(true);
+            spin(s);
+          }));
+      snprintf(k, sizeof k, "c702_%s_send_recv_spin_us", nm);
+      int cnt = 0;
+      put(k, median_us(iters, [&] {
+            msg(false);
+            // the ring is refilled every 256th message (outside the median: the ring never drains)
+            if (++cnt % 256 == 0 && cmpi_702_precompute(snd, 65535, 512, s) < 0) CM(-1);
+            spin(s);
+          }));
+      // throughput: 200 messages back to back, one wait at the end
+      snprintf(k, sizeof k, "c702_%s_send_precompute_recv_pipelined_us", nm);
+      put(k, median_us(std::max(20, iters / 50), [&] {
+            for (int i = 0; i < 200; ++i) msg(true);
+            spin(s);
+          }) / 200.0);
+      std::vector<uint8_t> a(n), b(n);
+      CK(hipMemcpy(a.data(), dpt, n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(b.data(), dbk, n, hipMemcpyDeviceToHost));
+      if (memcmp(a.data(), b.data(), n) || hdr[4] != '0') {
+        fprintf(stderr, "702 round trip failed (%zu, stream %c)\n", n, hdr[4]);
+        return 1;
+      }
+      CK(hipFree(dpt));
+      CK(hipFree(dct));
+      CK(hipFree(dbk));
+      CK(hipFree(dmask));
+    }
+    cmpi_702_sender_free(snd);
+    cmpi_ctx_free(cc);
+  }
   CK(hipHostFree(hflag));
   CK(hipStreamDestroy(s));
   printf("%s}\n", js.c_str());
