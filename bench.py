@@ -161,20 +161,20 @@ class OpenSSLRef:
         self.C.cb_ctr.restype = I
         self.threads = max(1, min(16, host_cpu_info()["usable"]))
 
-    def aead(self, alg: str, dec: bool, nonces: np.ndarray, inp: np.ndarray, n: int) -> tuple[np.ndarray, int]:
+    def aead(self, alg: str, dec: bool, nonces: np.ndarray, inp: np.ndarray, n: int, key: bytes = KEY):
         nrec = nonces.shape[0]
         nonces = np.ascontiguousarray(nonces, np.uint8)
         inp = np.ascontiguousarray(inp, np.uint8)
         out = np.zeros((nrec, n if dec else n + 16), np.uint8)
-        bad = self.C.cb_aead_batch(2 if alg == "ocb" else 1, 1 if dec else 0, KEY, nonces.ctypes.data, inp.ctypes.data,
+        bad = self.C.cb_aead_batch(2 if alg == "ocb" else 1, 1 if dec else 0, key, nonces.ctypes.data, inp.ctypes.data,
                                    inp.shape[1], out.ctypes.data, out.shape[1], n, nrec, self.threads)
         return out, bad
 
-    def ctr(self, ctr0: bytes, inp: np.ndarray) -> np.ndarray:
+    def ctr(self, ctr0: bytes, inp: np.ndarray, key: bytes = KEY) -> np.ndarray:
         inp = np.ascontiguousarray(inp, np.uint8)
         out = np.empty_like(inp)
         cb = (ctypes.c_uint8 * 16).from_buffer_copy(ctr0)
-        assert self.C.cb_ctr(KEY, cb, inp.ctypes.data, out.ctypes.data, inp.size, self.threads) == 0
+        assert self.C.cb_ctr(key, cb, inp.ctypes.data, out.ctypes.data, inp.size, self.threads) == 0
         return out
 
 
@@ -455,16 +455,43 @@ def copy_peak_gbs(device: int, nbytes: int = 1 << 30, reps: int = 10) -> float:
     return 2 * nbytes / best / 1e9
 
 
+def registered_host_buffer(nbytes: int) -> torch.Tensor:
+    """Page-locked host memory the way an MPI library registers a user buffer: anonymous memory,
+    2 MiB aligned, transparent huge pages requested (madvise MADV_HUGEPAGE), then hipHostRegister.
+    (torch pin_memory buffers DMA at the same peak but vary with the process's allocation history:
+    23-33 GiB/s for the pipelined seal in round-3 benches, tools/host_regress_probe.py.)  The
+    mapping lives as long as the process."""
+    libc = ctypes.CDLL(None)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    raw = libc.mmap(None, nbytes + (2 << 20), 3, 0x22, -1, 0)  # PROT_READ|WRITE, MAP_PRIVATE|ANONYMOUS
+    if raw in (None, ctypes.c_void_p(-1).value):
+        raise OSError("mmap failed")
+    base = (raw + (2 << 20) - 1) & ~((2 << 20) - 1)
+    libc.madvise(ctypes.c_void_p(base), nbytes, 14)  # MADV_HUGEPAGE (advice only)
+    a = np.frombuffer((ctypes.c_uint8 * nbytes).from_address(base), dtype=np.uint8)
+    a[:] = 0  # fault the pages in
+    from cryptmpi_2022_amd import _native as N
+
+    N.check(N.lib().cmpi_host_register(ctypes.c_void_p(base), nbytes))
+    return torch.from_numpy(a)
+
+
 def host_path_rate(device: int, n: int = 1024, nrec: int = 65536) -> dict:
     """PCIe-inclusive seal rates (the path starts and ends in host memory, BASELINE north_star):
     (a) pinned host -> H2D -> kernel -> D2H -> pinned host serialised on one stream;
-    (b) the library's host entry point cmpi_gcm_seal_host on pinned buffers (chunked 3-stream
-        pipeline, H2D / kernel / D2H overlapped); (c) the same on pageable buffers."""
+    (b) the library's host entry point cmpi_gcm_seal_host on page-locked buffers registered as an
+        MPI library registers user memory (registered_host_buffer; chunked 3-stream pipeline,
+        H2D / kernel / D2H overlapped), and the same on torch pin_memory buffers; (c) pageable."""
     from cryptmpi_2022_amd import _native as N
 
-    pt = torch.randint(0, 256, (nrec * n,), dtype=torch.uint8).pin_memory()
-    nonces = torch.randint(0, 256, (nrec * 12,), dtype=torch.uint8).pin_memory()
-    out = torch.empty(nrec * (n + 16), dtype=torch.uint8).pin_memory()
+    pt = registered_host_buffer(nrec * n)
+    pt.copy_(torch.randint(0, 256, (nrec * n,), dtype=torch.uint8))
+    nonces = registered_host_buffer(nrec * 12)
+    nonces.copy_(torch.randint(0, 256, (nrec * 12,), dtype=torch.uint8))
+    out = registered_host_buffer(nrec * (n + 16))
+    tp_pt, tp_n, tp_out = pt.clone().pin_memory(), nonces.clone().pin_memory(), out.clone().pin_memory()
     ctx = aead.AeadCtx(KEY, device=device)
     d_pt = torch.empty(nrec * n, dtype=torch.uint8, device=f"cuda:{device}")
     d_n = torch.empty(nrec * 12, dtype=torch.uint8, device=f"cuda:{device}")
@@ -498,8 +525,74 @@ def host_path_rate(device: int, n: int = 1024, nrec: int = 65536) -> dict:
     res = {"config": f"{nrec} x {n} B GCM seal, host buffers in and out",
            "pinned_serial_1stream_GiBps": round(rate(serial), 2),
            "host_api_pinned_pipelined_GiBps": round(rate(lambda: host_api(pt, out, nonces)), 2),
-           "host_api_pageable_GiBps": round(rate(lambda: host_api(pg_pt, pg_out, pg_n), 4), 2)}
+           "host_api_torch_pin_pipelined_GiBps": round(rate(lambda: host_api(tp_pt, tp_out, tp_n)), 2),
+           "host_api_pageable_GiBps": round(rate(lambda: host_api(pg_pt, pg_out, pg_n), 4), 2),
+           "pinned_buffers": "registered_host_buffer (2 MiB aligned, MADV_HUGEPAGE, cmpi_host_register)"}
     ctx.close()
+    return res
+
+
+def host602_rate(device: int, n: int = 8 << 20, reps: int = 8) -> dict:
+    """The 602 8 MiB message (mode '1': 16 outer messages of 512 KiB, 128 segments of 64 KiB,
+    per-message sub-key K' = AES_K(V) derived on the device) sealed from and opened into
+    page-locked host memory (registered_host_buffer), send.c:729-850 / recv.c:679-809:
+      seal_per_outer   one cmpi_602_seal_host_begin per outer message, all begun before the first
+                       wait (the reference seals outer k+1 while MPI_Isend of k is in flight);
+      seal_whole       the synchronous cmpi_602_seal_host of the whole message;
+      open_per_outer   one cmpi_602_open_host_begin per outer message, waited in order.
+    Best of `reps` after 3 warm-ups.  The wire is then checked against OpenSSL 3 (K' from
+    EVP_aes_128_ctr over V, every segment's GCM under "0000000"||flag||BE32(ctr)) and opened back."""
+    from cryptmpi_2022_amd import frame
+
+    plan = frame.plan602(n, 8, 0)
+    rand16 = bytes(range(16, 32))
+    header = frame.header602(plan, rand16)
+    master = aead.AeadCtx(KEY, device=device)
+    seg = aead.AeadCtx(bytes(16), device=device)
+    seg.rekey_subkey(master, header[4:20], stream=torch.cuda.current_stream(device))
+    torch.cuda.synchronize(device)
+    src = registered_host_buffer(n).numpy()
+    src[:] = np.random.default_rng(602).integers(0, 256, n, dtype=np.uint8)
+    wire = registered_host_buffer(plan.wire_bytes).numpy()
+    back = registered_host_buffer(n).numpy()
+
+    def seal_per_outer():
+        reqs = [frame.seal602_host_begin(seg, plan, header, wire, src, o) for o in range(plan.outer)]
+        for q in reqs:
+            q.wait()
+
+    def seal_whole():
+        frame.seal602_host(seg, plan, header, wire, src)
+
+    def open_per_outer():
+        reqs = [frame.open602_host_begin(seg, header, back, wire, o) for o in range(plan.outer)]
+        for q in reqs:
+            q.wait()
+
+    res = {"message_bytes": n, "plan": plan.as_dict(), "buffers": "registered_host_buffer (page-locked)"}
+    for name, fn in (("seal_per_outer", seal_per_outer), ("seal_whole", seal_whole), ("open_per_outer", open_per_outer)):
+        for _ in range(3):
+            fn()
+        best = float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            best = min(best, time.perf_counter() - t0)
+        res[name + "_GiBps"] = round(n / best / GIB, 2)
+    res["round_trip"] = bool(np.array_equal(back, src))
+    try:  # independent check of the wire: OpenSSL under K' = AES_K(V)
+        ref = OpenSSLRef()
+        kp = ref.ctr(header[4:20], np.zeros(16, np.uint8)).tobytes()
+        seg_len, nseg = plan.chop, plan.nseg
+        w = wire[: nseg * (seg_len + 21)].reshape(nseg, seg_len + 21)
+        nonces = np.concatenate([np.frombuffer(b"0000000", np.uint8)[None, :].repeat(nseg, 0), w[:, :5]], axis=1)
+        want, bad = ref.aead("gcm", False, nonces, src.reshape(nseg, seg_len), seg_len, key=kp)
+        res["parity_cpu"] = bad == 0 and bool(np.array_equal(w[:, 5:], want)) and plan.total == nseg * seg_len
+    except Exception as e:  # report, never hide
+        res["parity_cpu"] = {"error": repr(e)}
+    res["parity"] = "every segment's prefix-nonce, ciphertext and tag vs OpenSSL 3 under K' = AES_K(V)"
+    seg.close()
+    master.close()
     return res
 
 
@@ -1270,6 +1363,10 @@ def main() -> None:
             extras["host_path_pcie"] = host_path_rate(local)
         except Exception as e:
             extras["host_path_pcie"] = {"error": repr(e)}
+        try:
+            extras["host_602_8mib"] = host602_rate(local)
+        except Exception as e:
+            extras["host_602_8mib"] = {"error": repr(e)}
         for name, fn in (("async_host", lambda: async_host_rate(local)), ("ctr702", lambda: ctr702_rates(local)),
                          ("config1_exchange_64k", config1_exchange)):
             try:

@@ -173,6 +173,14 @@ cmpi::dev::RoundKeys folded(const cmpi::dev::RoundKeys& k) {
   return f;
 }
 
+// Events that only order device work after device work (hipStreamWaitEvent: a re-key before the
+// launches that read its tables, a scratch buffer's previous user, ring fills before the XOR that
+// consumes them, H2D before the kernel): a device-scope release, not the default system-scope
+// fence, whose cache writeback / invalidate left a ~5 us bubble before the next kernel of the
+// stream (702 send: ring XOR + event ~5.5 us over the launch floor, profiles/r04e_msg_latency.json).
+// Events the host waits on before reading host memory keep the default.
+constexpr unsigned kOrderEvent = hipEventDisableTiming | hipEventReleaseToDevice;
+
 // Order a launch on one of the library's streams after the context's last device re-key.
 int wait_keys(const cmpi_ctx* c, hipStream_t st) {
   if (!c->key_pending.load()) return CMPI_OK;
@@ -188,7 +196,7 @@ int wait_keys(const cmpi_ctx* c, hipStream_t st) {
 
 // After a re-key launched on `stream`: publish its completion event for wait_keys.
 int record_keys(const cmpi_ctx* c, hipStream_t stream) {
-  if (!c->key_ev) HIP_TRY(hipEventCreateWithFlags(&c->key_ev, hipEventDisableTiming));
+  if (!c->key_ev) HIP_TRY(hipEventCreateWithFlags(&c->key_ev, kOrderEvent));
   HIP_TRY(hipEventRecord(c->key_ev, stream));
   c->key_pending.store(true);
   return CMPI_OK;
@@ -288,7 +296,7 @@ struct ScratchLease {
     if (internal) return CMPI_OK;
     lk = std::unique_lock<std::mutex>(c->smu);
     internal = true;
-    if (!c->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
+    if (!c->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&c->scratch_ev, kOrderEvent));
     if (c->scratch_used) HIP_TRY(hipStreamWaitEvent(st, c->scratch_ev, 0));
     return CMPI_OK;
   }
@@ -979,8 +987,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   if (!P.init) {
     for (auto& st : P.s) HIP_TRY(lib_stream(&st));
     for (int i = 0; i < 4; ++i) {
-      HIP_TRY(hipEventCreateWithFlags(&P.in_ready[i], hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&P.k_done[i], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&P.in_ready[i], kOrderEvent));
+      HIP_TRY(hipEventCreateWithFlags(&P.k_done[i], kOrderEvent));
       HIP_TRY(hipEventCreateWithFlags(&P.slot_free[i], hipEventDisableTiming));
     }
     P.init = true;

@@ -96,7 +96,7 @@ int span_begin(const cmpi_ctx* c, size_t dev_bytes, const SpanIn& in, const Span
   if ((rc = wait_keys(c, st))) return bail(rc);
   if (order_after) {  // device work the call depends on, enqueued by the caller on its own stream
     hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(fail(CMPI_EHIP, "event create failed"));
+    if (hipEventCreateWithFlags(&e, kOrderEvent) != hipSuccess) return bail(fail(CMPI_EHIP, "event create failed"));
     const bool ok = hipEventRecord(e, after) == hipSuccess && hipStreamWaitEvent(st, e, 0) == hipSuccess;
     (void)hipEventDestroy(e);  // released once the wait is satisfied
     if (!ok) return bail(fail(CMPI_EHIP, "ordering after the caller's stream failed"));

@@ -159,10 +159,42 @@ __device__ __forceinline__ void gcm_nonce(const GcmArgs& a, uint32_t r, bool wri
 // LDS: GHASH byte table [v][p] @0 (64 KiB), AES row image @64K (64 KiB), nibble tables of
 // H^1..H^(L-1) @128K ((L-1) x 8 KiB; a lane whose weight is H^L multiplies by the byte table),
 // then the workgroup's progress counter (16 B, gcm_progress_prio).
+// The byte table is built in place from its 128 single-bit entries, staged first into a 2 KiB
+// basis area after the progress counter (build_byte_table).
 constexpr uint32_t kGcmRows = 65536u;
 constexpr uint32_t kGcmNib = 131072u;
 __host__ __device__ constexpr uint32_t gcm_prog_off(int L) { return kGcmNib + (uint32_t)(L - 1) * 8192u; }
-__host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return gcm_prog_off(L) + 16u; }
+__host__ __device__ constexpr uint32_t gcm_basis_off(int L) { return gcm_prog_off(L) + 16u; }
+__host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return gcm_basis_off(L) + 2048u; }
+
+// GHASH byte table [v][p] (entry (v, p) at dst + v*256 + p*16, the layout of gf128_host.hpp
+// build_byte_table) built in LDS from the global copy's 128 single-bit entries (v = 2^k):
+// entry (v, p) = XOR of the entries (2^k, p) over the set bits k of v (the table is linear in v).
+// 2 KiB leave L2 per workgroup instead of 64 KiB: with every CU staging at once the copy was
+// bound by L2 bandwidth (256 workgroups x 64 KiB).  Thread t builds position p = t & 15, values
+// 4m .. 4m+3 (m = t >> 4).  Ends with a barrier.
+__device__ __forceinline__ void build_byte_table(const u32x4* __restrict__ src, uint32_t dst, uint32_t basis) {
+  for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x) {  // basis[k][p] = entry (2^k, p)
+    const uint32_t k = i >> 4, p = i & 15u;
+    lds_st128(basis + i * 16u, src[(1u << k) * 16u + p]);
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < 1024u; t += blockDim.x) {
+    const uint32_t p = t & 15u, m = t >> 4;
+    u32x4 e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = lds128(basis + ((uint32_t)k * 16u + p) * 16u);
+    u32x4 b = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 2; k < 8; ++k)
+      if ((m >> (k - 2)) & 1u) b ^= e[k];
+    const uint32_t o = dst + 4u * m * 256u + p * 16u;
+    lds_st128(o, b);
+    lds_st128(o + 256u, b ^ e[0]);
+    lds_st128(o + 512u, b ^ e[1]);
+    lds_st128(o + 768u, b ^ e[0] ^ e[1]);
+  }
+}
 
 // Diagnostics build only (tools/Makefile, -DCMPI_TOOLS=1): per-workgroup wall-clock stamps of
 // the kernel phases (tools/probe_lane.py, tools/probe_flow.py).  The product library has none.
@@ -183,10 +215,10 @@ __host__ __device__ constexpr uint32_t gcm_lds_bytes(int L) { return gcm_prog_of
 template <int L, bool DECRYPT>
 __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
   CMPI_PROBE(a, 0u);
-  stage_copy(a.htab, 0u, 4096u);
   stage_rows(a.te0, kGcmRows);
   if (L > 1) stage_copy(a.ntab, kGcmNib, (uint32_t)(L - 1) * 512u);
   if (threadIdx.x == 0u) lds_st32(gcm_prog_off(L), 0u);
+  build_byte_table(a.htab, 0u, gcm_basis_off(L));
   __syncthreads();
   CMPI_PROBE(a, 1u);
 
@@ -574,8 +606,8 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
     uint32_t r = 0xffffffffu;
     if (u < units)  // wave-uniform
       pw = flow_unit<DECRYPT, DK>(a, rk, rl, lenblk, u, ub == blockIdx.x * wpb, va0, vb0, r);
-    if (DK || !a.one_wg) {  // partials for the combine launch
-      if (u < units && lane == 0u) a.partial[u] = pw;
+    if (DK || !a.one_wg) {  // partials for the combine launch, stored write-through like the records
+      if (u < units && lane == 0u) st_wt(wt_rsrc(reinterpret_cast<const uint8_t*>(a.partial)), 16u * u, pw);
       continue;
     }
     // one-workgroup batch (host-keyed): every chunk of every record is in this workgroup, so the

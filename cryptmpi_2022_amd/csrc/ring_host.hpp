@@ -82,7 +82,7 @@ cmpi_ctr_ring* cmpi_ctr_ring_new(const cmpi_ctx* ctx, const uint8_t iv[16], size
     delete r;
     return nullptr;
   }
-  if (hipEventCreateWithFlags(&r->last, hipEventDisableTiming) != hipSuccess) {
+  if (hipEventCreateWithFlags(&r->last, kOrderEvent) != hipSuccess) {
     fail(CMPI_EHIP, "hipEventCreate failed");
     (void)hipFree(r->dring);
     delete r;

@@ -20,7 +20,7 @@ SHAPES = {"8x1MiB": (1 << 20, 8), "1x64KiB": (65536, 1), "3x100000": (100000, 3)
           "32x256KiB": (256 << 10, 32), "8x(1MiB-5)": ((1 << 20) - 5, 8), "65536x1000": (1000, 65536),
           "1x1000": (1000, 1), "64x1000": (1000, 64), "2048x1000": (1000, 2048), "16x100": (100, 16),
           "1x100": (100, 1), "2048x600": (600, 2048), "2048x300": (300, 2048), "2048x200": (200, 2048),
-          "256x260": (260, 256), "16x300": (300, 16)}
+          "256x260": (260, 256), "16x300": (300, 16), "65536x1024": (1024, 65536), "65536x4096": (4096, 65536)}
 
 
 def child() -> None:
@@ -82,7 +82,7 @@ def main() -> None:
             s = sorted(r[name]["seal_us"] for r in runs[lib])
             o = sorted(r[name]["open_us"] for r in runs[lib])
             n, nrec = SHAPES[name]
-            row[os.path.basename(lib)] = {"seal_us": round(s[len(s) // 2], 2), "open_us": round(o[len(o) // 2], 2),
+            row[os.path.basename(os.path.dirname(os.path.abspath(lib))) + '/' + os.path.basename(lib)] = {"seal_us": round(s[len(s) // 2], 2), "open_us": round(o[len(o) // 2], 2),
                                           "seal_GiBps": round(n * nrec / (s[len(s) // 2] * 1e-6) / (1 << 30), 1),
                                           "ok": all(r[name]["ok"] for r in runs[lib])}
         row["same_ct"] = len({r[name]["ct_sha"] for lib in libs for r in runs[lib]}) == 1

@@ -335,6 +335,58 @@ int main(int argc, char** argv) {
             if (++cnt % 256 == 0 && cmpi_702_precompute(snd, 65535, 512, s) < 0) CM(-1);
             spin(s);
           }));
+      // the same with the host spinning on a page-locked word a one-wave kernel writes after the
+      // message's kernels (the completion floor is 6 us there, 13 us with hipStreamQuery polling)
+      auto flag_wait = [&] {
+        ++seq;
+        flag_kernel<<<1, 64, 0, s>>>(dflag, seq);
+        while (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) != seq) {
+        }
+      };
+      cnt = 0;
+      snprintf(k, sizeof k, "c702_%s_send_premask_recv_flag_us", nm);
+      put(k, median_us(iters, [&] {
+            msg(false);
+            if (++cnt % 256 == 0 && cmpi_702_precompute(snd, 65535, 512, s) < 0) CM(-1);
+            flag_wait();
+          }));
+      cnt = 0;
+      snprintf(k, sizeof k, "c702_%s_send_recv_nomask_flag_us", nm);  // payload landed first: direct CTR
+      put(k, median_us(iters, [&] {
+            if (cmpi_702_send(snd, 0, dpt, n, hdr, dct, s) < 1) CM(-1);
+            CM(cmpi_702_recv(cc, iv, hdr, dbk, n, dct, nullptr, 0, s));
+            if (++cnt % 256 == 0 && cmpi_702_precompute(snd, 65535, 512, s) < 0) CM(-1);
+            flag_wait();
+          }));
+      cnt = 0;
+      snprintf(k, sizeof k, "c702_%s_send_only_flag_us", nm);
+      put(k, median_us(iters, [&] {
+            if (cmpi_702_send(snd, 0, dpt, n, hdr, dct, s) < 1) CM(-1);
+            if (++cnt % 256 == 0 && cmpi_702_precompute(snd, 65535, 512, s) < 0) CM(-1);
+            flag_wait();
+          }));
+      // host CPU time of the calls alone (the stream drained every 64 calls, outside the median)
+      cnt = 0;
+      snprintf(k, sizeof k, "c702_%s_send_call_cpu_us", nm);
+      put(k, median_us(iters, [&] {
+            if (++cnt % 64 == 0) {
+              if (cmpi_702_precompute(snd, 65535, 512, s) < 0) CM(-1);
+              spin(s);
+              return;
+            }
+            if (cmpi_702_send(snd, 0, dpt, n, hdr, dct, s) < 1) CM(-1);
+          }));
+      spin(s);
+      cnt = 0;
+      snprintf(k, sizeof k, "c702_%s_recv_direct_call_cpu_us", nm);
+      put(k, median_us(iters, [&] {
+            if (++cnt % 64 == 0) {
+              spin(s);
+              return;
+            }
+            CM(cmpi_702_recv(cc, iv, hdr, dbk, n, dct, nullptr, 0, s));
+          }));
+      spin(s);
       // throughput: 200 messages back to back, one wait at the end
       snprintf(k, sizeof k, "c702_%s_send_precompute_recv_pipelined_us", nm);
       put(k, median_us(std::max(20, iters / 50), [&] {
