@@ -4,6 +4,8 @@ single 64 KiB messages, 3 x 100000 B, 1 x 8 MiB, 32 x 256 KiB) and two ragged on
 65536 x 1000 B on the lane kernel) and short records (1000 B, 100 B; few of them).
 
     python tools/flow_ab.py <libA.so> <libB.so> [rounds]
+    (a build may carry test hooks: path/libcmpi_aead.so@lane_aligned=0 calls
+     cmpi_debug_set_lane_aligned(0) in that build's processes)
 
 Each (round, build) runs in its own process (`--child <lib>`): per shape, 0.3 s of warm-up, then
 seal and open kernel times from fence-free HIP events over 30 back-to-back calls; the parent prints
@@ -28,6 +30,11 @@ def child() -> None:
     import torch
 
     import bench
+    from cryptmpi_2022_amd import _native as N
+
+    for kv in filter(None, os.environ.get("AB_HOOKS", "").split(",")):
+        k, v = kv.split("=")
+        getattr(N.lib(), "cmpi_debug_set_" + k)(int(v))
 
     out = {}
     for name, (n, nrec) in SHAPES.items():
@@ -68,7 +75,8 @@ def main() -> None:
     runs = {lib: [] for lib in libs}
     for _ in range(rounds):
         for lib in libs:
-            env = dict(os.environ, CMPI_LIB=os.path.abspath(lib))
+            path, _, hooks = lib.partition("@")
+            env = dict(os.environ, CMPI_LIB=os.path.abspath(path), AB_HOOKS=hooks)
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib], env=env,
                                capture_output=True, text=True, timeout=120)
             if p.returncode != 0:
@@ -82,7 +90,7 @@ def main() -> None:
             s = sorted(r[name]["seal_us"] for r in runs[lib])
             o = sorted(r[name]["open_us"] for r in runs[lib])
             n, nrec = SHAPES[name]
-            row[os.path.basename(os.path.dirname(os.path.abspath(lib))) + '/' + os.path.basename(lib)] = {"seal_us": round(s[len(s) // 2], 2), "open_us": round(o[len(o) // 2], 2),
+            row[os.path.basename(os.path.dirname(os.path.abspath(lib.partition("@")[0]))) + "/" + os.path.basename(lib)] = {"seal_us": round(s[len(s) // 2], 2), "open_us": round(o[len(o) // 2], 2),
                                           "seal_GiBps": round(n * nrec / (s[len(s) // 2] * 1e-6) / (1 << 30), 1),
                                           "ok": all(r[name]["ok"] for r in runs[lib])}
         row["same_ct"] = len({r[name]["ct_sha"] for lib in libs for r in runs[lib]}) == 1

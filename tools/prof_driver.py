@@ -18,6 +18,11 @@ ap.add_argument("--seal-only", action="store_true")
 ap.add_argument("--out-stride", type=int, default=0,
                 help="gcm1k seal-only traffic calibration: output record stride (0 = dense n+16)")
 a = ap.parse_args()
+for kv in filter(None, os.environ.get("AB_HOOKS", "").split(",")):  # test hooks, e.g. lane_aligned=0
+    from cryptmpi_2022_amd import _native as _N
+
+    k, v = kv.split("=")
+    getattr(_N.lib(), "cmpi_debug_set_" + k)(int(v))
 if a.out_stride:  # 65 536 x 1 KiB seals into records `out_stride` bytes apart (aligned vs dense)
     from cryptmpi_2022_amd import aead
 
