@@ -12,6 +12,9 @@
  * 16-byte rounding, the -1024 head-room guard), so the bytes produced equal the reference's for
  * the same call sequence.  Counter block of counter c = IV_Count(iv, c) (send.c:1019-1030).
  * Calls on one ring must be stream-ordered by the caller (generate and encrypt touch the ring).
+ * Calls on different streams are ordered by the library (an event recorded on the previous
+ * call's stream when the stream changes); the stream of a ring's (or 702 sender's) last call must
+ * stay valid until its next call on another stream, or until the ring / sender is freed.
  */
 #ifndef CMPI_RING_H
 #define CMPI_RING_H

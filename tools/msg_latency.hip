@@ -17,6 +17,9 @@
 #include "../include/cmpi_aead.h"
 #include "../include/cmpi_debug.h"
 #include "../include/cmpi_ctrmode.h"
+#include "../include/cmpi_ring.h"
+#include "../include/cmpi_frame.h"
+#include "../include/cmpi_async.h"
 #include "../include/cmpi_service.h"
 
 #define CK(x)                                                                            \
@@ -365,6 +368,39 @@ int main(int argc, char** argv) {
             if (++cnt % 256 == 0 && cmpi_702_precompute(snd, 65535, 512, s) < 0) CM(-1);
             flag_wait();
           }));
+      // the kernels alone, each followed by the flag kernel: a 4 KiB XOR (cmpi_xor_bytes), a 4 KiB
+      // CTR keystream XOR (cmpi_ctr_xor), and an event record between two flag kernels
+      snprintf(k, sizeof k, "c702_%s_xor_kernel_flag_us", nm);
+      put(k, median_us(iters, [&] {
+            CM(cmpi_xor_bytes(dbk, dct, dpt, n, s));
+            flag_wait();
+          }));
+      uint8_t ctr0[16] = {0};
+      snprintf(k, sizeof k, "c702_%s_ctr_kernel_flag_us", nm);
+      put(k, median_us(iters, [&] {
+            CM(cmpi_ctr_xor(cc, dbk, dct, n, ctr0, s));
+            flag_wait();
+          }));
+      snprintf(k, sizeof k, "c702_%s_two_ctr_kernels_flag_us", nm);
+      put(k, median_us(iters, [&] {
+            CM(cmpi_ctr_xor(cc, dbk, dct, n, ctr0, s));
+            CM(cmpi_ctr_xor(cc, dmask, dct, n, ctr0, s));
+            flag_wait();
+          }));
+      {
+        hipEvent_t e1;
+        CK(hipEventCreateWithFlags(&e1, hipEventDisableTiming | hipEventReleaseToDevice));
+        snprintf(k, sizeof k, "c702_%s_xor_event_flag_us", nm);
+        put(k, median_us(iters, [&] {
+              CM(cmpi_xor_bytes(dbk, dct, dpt, n, s));
+              CK(hipEventRecord(e1, s));
+              flag_wait();
+            }));
+        snprintf(k, sizeof k, "event_record_cpu_us");
+        put(k, median_us(iters, [&] { CK(hipEventRecord(e1, s)); }));
+        spin(s);
+        CK(hipEventDestroy(e1));
+      }
       // host CPU time of the calls alone (the stream drained every 64 calls, outside the median)
       cnt = 0;
       snprintf(k, sizeof k, "c702_%s_send_call_cpu_us", nm);
@@ -407,6 +443,54 @@ int main(int argc, char** argv) {
     }
     cmpi_702_sender_free(snd);
     cmpi_ctx_free(cc);
+  }
+  {  // 602: an 8 MiB message from / into page-locked memory, one request per outer message
+     // (send.c:729-850, recv.c:679-809): CPU time of the 16 *_begin calls and the whole message
+    uint8_t mkey[16];
+    for (int i = 0; i < 16; ++i) mkey[i] = (uint8_t)(7 * i);
+    cmpi_ctx* master = cmpi_ctx_new(CMPI_AES_128_GCM, mkey, 16, 16, 0);
+    const uint32_t n = 8u << 20;
+    cmpi_602_plan plan;
+    CM(cmpi_602_plan_make(n, 8, 0, &plan));
+    uint8_t rnd[16], hdr[25];
+    for (int i = 0; i < 16; ++i) rnd[i] = (uint8_t)(i + 16);
+    CM(cmpi_602_header(&plan, rnd, hdr));
+    cmpi_ctx* seg = cmpi_ctx_derive_subkey(master, hdr + 4, s);
+    if (!master || !seg) {
+      fprintf(stderr, "602 contexts: %s\n", cmpi_last_error());
+      return 1;
+    }
+    CK(hipStreamSynchronize(s));
+    uint8_t *src, *wire, *back;
+    CK(hipHostMalloc((void**)&src, n, hipHostMallocDefault));
+    CK(hipHostMalloc((void**)&wire, plan.wire_bytes, hipHostMallocDefault));
+    CK(hipHostMalloc((void**)&back, n, hipHostMallocDefault));
+    for (uint32_t i = 0; i < n; ++i) src[i] = (uint8_t)(i * 13 + 1);
+    std::vector<cmpi_req*> rq(plan.outer);
+    double begin_us = 0;
+    auto seal_outer = [&] {
+      const double a = now_us();
+      for (uint32_t o = 0; o < plan.outer; ++o) CM(cmpi_602_seal_host_begin(seg, &plan, hdr, wire, src, o, 1, &rq[o]));
+      begin_us = now_us() - a;
+      CM(cmpi_waitall(rq.data(), rq.size()));
+    };
+    const int it602 = std::max(20, iters / 50);
+    put("c602_8m_seal_per_outer_us", median_us(it602, seal_outer));
+    put("c602_8m_seal_16_begins_cpu_us", begin_us);
+    put("c602_8m_open_per_outer_us", median_us(it602, [&] {
+          for (uint32_t o = 0; o < plan.outer; ++o) CM(cmpi_602_open_host_begin(seg, hdr, back, wire, o, 1, nullptr, &rq[o]));
+          CM(cmpi_waitall(rq.data(), rq.size()));
+        }));
+    put("c602_8m_seal_whole_us", median_us(it602, [&] { CM(cmpi_602_seal_host(seg, &plan, hdr, wire, src)); }));
+    if (memcmp(src, back, n)) {
+      fprintf(stderr, "602 round trip failed\n");
+      return 1;
+    }
+    CK(hipHostFree(src));
+    CK(hipHostFree(wire));
+    CK(hipHostFree(back));
+    cmpi_ctx_free(seg);
+    cmpi_ctx_free(master);
   }
   CK(hipHostFree(hflag));
   CK(hipStreamDestroy(s));
