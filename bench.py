@@ -1109,6 +1109,33 @@ def ctr702_rates(device: int, steps: int = 50) -> dict:
     return res
 
 
+def c_timed_latency(iters: int = 300) -> dict:
+    """Per-message latencies timed from C (tools/msg_latency: no Python on the path), medians of
+    `iters` calls: device-resident 702 4 KiB messages (send.c:1537-1731 / recv.c:1107-1220; the
+    host spins on a word a one-wave kernel writes after the message), single GCM messages through
+    the resident service, and the 602 8 MiB message from page-locked memory."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "msg_latency")
+    if not os.path.exists(exe):
+        return {"error": "tools/msg_latency not built (make -C tools msg_latency)"}
+    p = subprocess.run([exe, str(iters)], capture_output=True, text=True, timeout=240)
+    if p.returncode != 0:
+        return {"error": p.stderr[-400:]}
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    keep = ("flag_kernel_host_spin_us", "c702_4k_send_only_flag_us", "c702_4k_send_recv_nomask_flag_us",
+            "c702_4k_send_premask_recv_flag_us", "c702_4k_send_precompute_recv_pipelined_us",
+            "c702_4k_send_call_cpu_us", "c702_4k_recv_direct_call_cpu_us", "svc_pinned_seal_1k_us",
+            "svc_pinned_open_1k_us", "svc_pinned_seal_64k_us", "svc_pinned_open_64k_us", "c602_8m_seal_per_outer_us",
+            "c602_8m_seal_whole_us", "c602_8m_open_per_outer_us")
+    out = {k: d[k] for k in keep if k in d}
+    for k in ("c602_8m_seal_per_outer_us", "c602_8m_seal_whole_us", "c602_8m_open_per_outer_us"):
+        if k in d:
+            out[k.replace("_us", "_GiBps")] = round((8 << 20) / (d[k] * 1e-6) / GIB, 2)
+    out["iters"] = iters
+    return out
+
+
 def cpu_port_baseline(workload: str, seconds: float = 4.0) -> dict:
     """Secondary CPU datum: the oracle's C restatement (portable table AES, bit-serial GHASH;
     oracle/liboracle.so), all usable host threads, on a bounded sample of the workload."""
@@ -1368,7 +1395,7 @@ def main() -> None:
         except Exception as e:
             extras["host_602_8mib"] = {"error": repr(e)}
         for name, fn in (("async_host", lambda: async_host_rate(local)), ("ctr702", lambda: ctr702_rates(local)),
-                         ("config1_exchange_64k", config1_exchange)):
+                         ("config1_exchange_64k", config1_exchange), ("c_timed_latency", c_timed_latency)):
             try:
                 extras[name] = fn()
             except Exception as e:  # report, never hide
