@@ -511,6 +511,57 @@ __device__ __forceinline__ u32x4 shfl_xor4(u32x4 v, int m) {
   return r;
 }
 
+// XOR exchanges across lanes without the LDS crossbar (all 64 lanes active).  __shfl_xor
+// compiles to ds_bpermute_b32: an LDS round trip per dword and step, which made the flow
+// kernel's lane tree and chunk weight (56 of them in sequence-dependent groups) a latency chain.
+// DPP row ops and gfx950's v_permlane16/32_swap are plain VALU:
+//   xq1 / xq2   x ^ x[l ^ 1] / x ^ x[l ^ 2]        (quad_perm)
+//   xr4 / xr8   x ^ x[l - 4] / x ^ x[l - 8] within a row of 16 (row_ror; applied in turn they sum
+//               the four lanes l mod 4 of a row, as xor 4 then xor 8 do)
+//   x16 / x32   x ^ x[l ^ 16] / x ^ x[l ^ 32]      (permlane16 / permlane32 swap, the pair XORed)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ u32x4 xq1(u32x4 v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] ^= dpp_mov<0xB1>(v[c]);  // quad_perm [1,0,3,2]
+  return v;
+}
+__device__ __forceinline__ u32x4 xq2(u32x4 v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] ^= dpp_mov<0x4E>(v[c]);  // quad_perm [2,3,0,1]
+  return v;
+}
+__device__ __forceinline__ u32x4 xr4(u32x4 v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] ^= dpp_mov<0x124>(v[c]);  // row_ror:4
+  return v;
+}
+__device__ __forceinline__ u32x4 xr8(u32x4 v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] ^= dpp_mov<0x128>(v[c]);  // row_ror:8 (= lane ^ 8 in a row)
+  return v;
+}
+__device__ __forceinline__ u32x4 x16(u32x4 v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v[c], v[c], false, false);
+    v[c] = r[0] ^ r[1];
+  }
+  return v;
+}
+__device__ __forceinline__ u32x4 x32(u32x4 v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v[c], v[c], false, false);
+    v[c] = r[0] ^ r[1];
+  }
+  return v;
+}
+// XOR of all 64 lanes, in every lane.
+__device__ __forceinline__ u32x4 xor_all_lanes(u32x4 v) { return x32(x16(xr8(xr4(xq2(xq1(v)))))); }
+
 // Y · M for wave-uniform Y and M, computed by the whole wavefront (all 64 lanes active):
 // Y·M = XOR_k m_k · (Y·x^k); lane l takes the coefficients k = 2l, 2l+1 of M (one variable
 // shift gf_mulx_pow and one single shift), and the 64 lane terms are XOR-reduced with
@@ -533,8 +584,7 @@ __device__ __forceinline__ u32x4 gmul_wave(u32x4 y, u32x4 m) {
   zh ^= yh & b1;
   zl ^= yl & b1;
   u32x4 z = gf_join(zh, zl);
-#pragma unroll
-  for (int s = 1; s < 64; s <<= 1) z ^= shfl_xor4(z, s);
+  z = xor_all_lanes(z);
   return z;
 }
 
@@ -561,8 +611,7 @@ __device__ __forceinline__ u32x4 gmul_wave4(const u32x4 (&y)[4], const u32x4 (&m
     zl ^= yl & b1;
   }
   u32x4 z = gf_join(zh, zl);
-#pragma unroll
-  for (int s = 1; s < 64; s <<= 1) z ^= shfl_xor4(z, s);
+  z = xor_all_lanes(z);
   return z;
 }
 

@@ -390,7 +390,8 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     // 2^16 / G chunks instead of one extra 1-block chunk that would start a second round.
     // 512-thread workgroups, one per CU (228 VGPRs, no spills; 8 x 1 MiB at S = 4: 22.6 us vs
     // 30.9 at 1024 threads): a round is 8 waves per CU
-    const uint64_t W = (uint64_t)c->ncu * 8;
+    const int fnt = g_flow_nt.load();
+    const uint64_t W = (uint64_t)c->ncu * (fnt ? (uint64_t)fnt / 64 : 8);
     const uint64_t smax = std::max<uint64_t>(1, nx / 64);
     uint64_t S = g_force_S.load();
     if (!S) {
@@ -413,7 +414,7 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     // few waves (single messages, the 600/EVP regime; the naive alltoall's 8 x 1 MiB): 512-thread
     // workgroups (1 x 64 KiB seal 21.0 -> 15.7 us at S = 2)
     if ((uint64_t)nrec * p.nseg <= (uint64_t)c->ncu * 8) p.nt = 512;
-    if (g_flow_nt.load()) p.nt = (uint32_t)g_flow_nt.load();
+    if (fnt) p.nt = (uint32_t)fnt;
     return p;
   }
   uint64_t G = (nx + nseg - 1) / nseg;

@@ -314,8 +314,8 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
       else f = gmul_nib(acc, kGcmNib + (w - 1u) * 8192u);
     }
     if (a.nseg == 1) f ^= ekj0;
-#pragma unroll
-    for (int m = 1; m < L; m <<= 1) f ^= shfl_xor4(f, m);
+    if (L > 1) f = xq1(f);
+    if (L > 2) f = xq2(f);
 
     if (a.nseg > 1) {
       if (q == 0) a.partial[g] = f;
@@ -430,23 +430,20 @@ __device__ __forceinline__ u32x4 flow_tree_r4(u32x4 acc, uint32_t lane) {
     asm volatile("" : "+v"(tb)::"memory");
     x = gmul_nib(x, tb);
   }
-  x ^= shfl_xor4(x, 16);
-  x ^= shfl_xor4(x, 32);  // every lane t: A_(t & 15)
+  x = x32(x16(x));  // every lane t: A_(t & 15)
   x = shfl4(x, 4u * (lane & 3u) + ((lane >> 2) & 3u));
   if (lane < 12u) {
     uint32_t tb = flow_tab(5u - (lane >> 2));
     asm volatile("" : "+v"(tb)::"memory");
     x = gmul_nib(x, tb);
   }
-  x ^= shfl_xor4(x, 4);
-  x ^= shfl_xor4(x, 8);  // lanes t < 16: B_(t & 3)
+  x = xr8(xr4(x));  // lanes t < 16: B_(t & 3)
   if (lane < 3u) {
     uint32_t tb = flow_tab(8u - lane);
     asm volatile("" : "+v"(tb)::"memory");
     x = gmul_nib(x, tb);
   }
-  x ^= shfl_xor4(x, 1);
-  x ^= shfl_xor4(x, 2);  // lane 0: V
+  x = xq2(xq1(x));  // lane 0: V
   return x;
 }
 
@@ -712,8 +709,7 @@ __global__ __launch_bounds__(256) void gcm_combine_kernel(GcmCombineArgs a) {
         if ((lane >> j) & 1u) y = q;
       }
     }
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) y ^= shfl_xor4(y, m);
+    y = xor_all_lanes(y);
     if (a.ekj0) y ^= a.ekj0[r];  // null: E_K(J0) already inside the partials
     if (!DECRYPT) {
       if (lane == 0u) st_blk(a.out + (uint64_t)r * a.out_stride + a.len, y);
@@ -752,8 +748,7 @@ __global__ __launch_bounds__(256) void gcm_xor_combine_kernel(GcmCombineArgs a) 
   }
   for (; k < a.nseg; k += 256u) y[0] ^= part[k];
   u32x4 v = y[0] ^ y[1] ^ y[2] ^ y[3];
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) v ^= shfl_xor4(v, m);
+  v = xor_all_lanes(v);
   if (lane == 0u) lds_st128((t >> 6) * 16u, v);
   __syncthreads();
   if (t == 0u) {

@@ -202,8 +202,7 @@ __global__ __launch_bounds__(1024, DECRYPT ? 4 : 8) void ocb_batch_kernel(OcbArg
       U ^= L5 ^ ocb_l(LB, 2u + 6u + (uint32_t)__builtin_ctz(k + 1u));
       vcur = vnext;
     }
-#pragma unroll
-    for (int msk = 1; msk < 64; msk <<= 1) csum ^= shfl_xor4(csum, msk);
+    csum = xor_all_lanes(csum);
     if (lane == 0) a.partial[item] = csum;
     __syncthreads();  // the Offset_0 slots are rewritten by the next round
   }

@@ -35,7 +35,7 @@ int cmpi_debug_event_record(void* ev, void* stream);
 float cmpi_debug_event_ms(void* a, void* b);
 void cmpi_debug_event_free(void* ev);
 /* gcm_flow_kernel threads per workgroup: 0 automatic (512 when the batch is at most 8 waves per
- * CU, else 1024), 512 or 1024 forced. */
+ * CU, else 1024), 512 or 1024 forced (the chunk plan then assumes that many waves per CU). */
 void cmpi_debug_set_flow_threads(int threads);
 /* FLOW kernel: a batch whose chunks all fit one workgroup finishes its tags in-kernel (1, default)
  * or through the XOR-combine launch (0). */

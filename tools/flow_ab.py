@@ -90,7 +90,9 @@ def main() -> None:
             s = sorted(r[name]["seal_us"] for r in runs[lib])
             o = sorted(r[name]["open_us"] for r in runs[lib])
             n, nrec = SHAPES[name]
-            row[os.path.basename(os.path.dirname(os.path.abspath(lib.partition("@")[0]))) + "/" + os.path.basename(lib)] = {"seal_us": round(s[len(s) // 2], 2), "open_us": round(o[len(o) // 2], 2),
+            path, _, hooks = lib.partition("@")
+            key = os.path.basename(os.path.dirname(os.path.abspath(path))) + "/" + os.path.basename(path)
+            row[key + ("@" + hooks if hooks else "")] = {"seal_us": round(s[len(s) // 2], 2), "open_us": round(o[len(o) // 2], 2),
                                           "seal_GiBps": round(n * nrec / (s[len(s) // 2] * 1e-6) / (1 << 30), 1),
                                           "ok": all(r[name]["ok"] for r in runs[lib])}
         row["same_ct"] = len({r[name]["ct_sha"] for lib in libs for r in runs[lib]}) == 1
