@@ -1111,9 +1111,12 @@ def ctr702_rates(device: int, steps: int = 50) -> dict:
 
 def c_timed_latency(iters: int = 300) -> dict:
     """Per-message latencies timed from C (tools/msg_latency: no Python on the path), medians of
-    `iters` calls: device-resident 702 4 KiB messages (send.c:1537-1731 / recv.c:1107-1220; the
-    host spins on a word a one-wave kernel writes after the message), single GCM messages through
-    the resident service, and the 602 8 MiB message from page-locked memory."""
+    `iters` calls: device-resident 702 4 KiB messages (send.c:1537-1731 / recv.c:1107-1220), with
+    a launch per op (the host spins on a word a one-wave kernel writes after the message) and
+    served by the CTR context's resident service (each call complete on return: send, and the
+    receiver's XOR once the payload has landed — its premask runs while the payload is in flight,
+    recv.c:1107-1196); single GCM messages through the resident service; and the 602 8 MiB
+    message from page-locked memory."""
     import subprocess
 
     exe = os.path.join(ROOT, "tools", "msg_latency")
@@ -1125,13 +1128,17 @@ def c_timed_latency(iters: int = 300) -> dict:
     d = json.loads(p.stdout.strip().splitlines()[-1])
     keep = ("flag_kernel_host_spin_us", "c702_4k_send_only_flag_us", "c702_4k_send_recv_nomask_flag_us",
             "c702_4k_send_premask_recv_flag_us", "c702_4k_send_precompute_recv_pipelined_us",
-            "c702_4k_send_call_cpu_us", "c702_4k_recv_direct_call_cpu_us", "svc_pinned_seal_1k_us",
+            "c702_4k_send_call_cpu_us", "c702_4k_recv_direct_call_cpu_us", "c702_4k_served_send_only_us",
+            "c702_4k_served_recv_mask_us", "c702_4k_served_send_recv_nomask_us",
+            "c702_4k_served_send_premask_recv_us", "svc_pinned_seal_1k_us",
             "svc_pinned_open_1k_us", "svc_pinned_seal_64k_us", "svc_pinned_open_64k_us", "c602_8m_seal_per_outer_us",
             "c602_8m_seal_whole_us", "c602_8m_open_per_outer_us")
     out = {k: d[k] for k in keep if k in d}
     for k in ("c602_8m_seal_per_outer_us", "c602_8m_seal_whole_us", "c602_8m_open_per_outer_us"):
         if k in d:
             out[k.replace("_us", "_GiBps")] = round((8 << 20) / (d[k] * 1e-6) / GIB, 2)
+    if "c702_4k_served_send_only_us" in d and "c702_4k_served_recv_mask_us" in d:
+        out["c702_4k_served_send_plus_recv_us"] = round(d["c702_4k_served_send_only_us"] + d["c702_4k_served_recv_mask_us"], 2)
     out["iters"] = iters
     return out
 

@@ -68,6 +68,20 @@ class _Ctx:
     def handle(self):
         return self._h
 
+    # ------------------------------------------------------------ resident message service
+    def service_start(self, idle_us: int = 0) -> None:
+        """Serve this context's single host messages (GCM: seal_host/open_host with nrec = 1,
+        <= 512 KiB; CTR: the 700 / 702 ops of messages <= 64 KiB, synchronously) from a resident
+        kernel (include/cmpi_service.h); it returns its CUs after `idle_us` (0 = 2000) without a
+        message and restarts on the next."""
+        N.check(N.lib().cmpi_service_start(self._h, idle_us))
+
+    def service_stop(self) -> None:
+        N.check(N.lib().cmpi_service_stop(self._h))
+
+    def service_running(self) -> bool:
+        return bool(N.lib().cmpi_service_running(self._h))
+
 
 class AeadCtx(_Ctx):
     """AES-128-GCM (default) or AES-128-OCB AEAD context: 12-byte nonce, 16-byte tag, no AAD."""
@@ -107,19 +121,6 @@ class AeadCtx(_Ctx):
         """Re-key this GCM context in place to K' = AES_K(V) on `stream` (no allocation)."""
         vb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(v))
         N.check(N.lib().cmpi_ctx_rekey_subkey(self._h, base.handle, vb, _stream_ptr(stream)))
-
-    # ------------------------------------------------------------ resident message service
-    def service_start(self, idle_us: int = 0) -> None:
-        """Serve this context's single host messages (seal_host/open_host with nrec = 1,
-        <= 512 KiB) from a resident kernel (include/cmpi_service.h); it returns its CUs after
-        `idle_us` (0 = 2000) without a message and restarts on the next."""
-        N.check(N.lib().cmpi_service_start(self._h, idle_us))
-
-    def service_stop(self) -> None:
-        N.check(N.lib().cmpi_service_stop(self._h))
-
-    def service_running(self) -> bool:
-        return bool(N.lib().cmpi_service_running(self._h))
 
     # ------------------------------------------------------------ device-resident batches
     def seal_batch(self, out, inp, nonces, length: int, nrec: int, *, in_stride=None, out_stride=None,

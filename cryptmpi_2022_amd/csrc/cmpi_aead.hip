@@ -17,6 +17,7 @@
 #include <array>
 #include <map>
 #include <memory>
+#include <optional>
 #include <mutex>
 #include <string>
 #include <thread>

@@ -42,9 +42,9 @@ void add128_host(uint8_t cb[16], uint64_t k) {
 }
 
 // out[off..off+len) = in ^ keystream (in == nullptr: keystream) per slice, consecutive counter
-// blocks merged into one launch.
+// blocks merged into one launch (or one served op: sv, begun).
 int ctr_slices(const cmpi_ctx* c, const uint8_t iv[16], const std::vector<CtrSlice>& v, uint8_t* out,
-               const uint8_t* in, void* stream) {
+               const uint8_t* in, void* stream, Served* sv = nullptr) {
   size_t i = 0;
   while (i < v.size()) {
     uint8_t cb[16], next[16];
@@ -61,7 +61,8 @@ int ctr_slices(const cmpi_ctx* c, const uint8_t iv[16], const std::vector<CtrSli
       ++j;
       len += v[j].len;
     }
-    const int rc = ctr_launch(c, out + v[i].off, in ? in + v[i].off : nullptr, len, cb, stream);
+    const int rc = sv ? sv->ctr(out + v[i].off, in ? in + v[i].off : nullptr, len, cb)
+                      : ctr_launch(c, out + v[i].off, in ? in + v[i].off : nullptr, len, cb, stream);
     if (rc) return rc;
     i = j + 1;
   }
@@ -123,7 +124,15 @@ int cmpi_700_send(const cmpi_ctx* c, const uint8_t send_iv[16], uint64_t* counte
   uint8_t iv[16];
   memcpy(iv, send_iv, 16);
   cmpi_iv_count(iv, (unsigned long)*counter);       // :983-986 (one segment)
-  const int rc = n ? ctr_launch(c, out, in, n, iv, stream) : CMPI_OK;
+  int rc = CMPI_OK;
+  if (n) {
+    Served sv(c, n);
+    if (sv) {
+      if (!(rc = sv.begin(stream))) rc = sv.ctr(out, in, n, iv);
+    } else {
+      rc = ctr_launch(c, out, in, n, iv, stream);
+    }
+  }
   if (rc) return rc;
   *counter += (unsigned long)(totaldata - 1) / 16 + 1;  // :1005
   return CMPI_OK;
@@ -139,7 +148,11 @@ int cmpi_700_recv(const cmpi_ctx* c, const uint8_t recv_iv[16], const uint8_t he
   uint8_t iv[16];
   memcpy(iv, recv_iv, 16);
   cmpi_iv_count(iv, be32h(header + 5));  // recv.c:867-871
-  return totaldata ? ctr_launch(c, out, in, totaldata, iv, stream) : CMPI_OK;
+  if (!totaldata) return CMPI_OK;
+  Served sv(c, totaldata);
+  if (!sv) return ctr_launch(c, out, in, totaldata, iv, stream);
+  if (int rc = sv.begin(stream)) return rc;
+  return sv.ctr(out, in, totaldata, iv);
 }
 
 cmpi_702_sender* cmpi_702_sender_new(const cmpi_ctx* c, const uint8_t send_iv[32], size_t ring_bytes,
@@ -228,14 +241,16 @@ int cmpi_702_send(cmpi_702_sender* s, int pending, const uint8_t* in, size_t n, 
   DeviceGuard dg(s->ctx->device);
   int rc;
   if (totaldata < kPreCom) {  // :1689-1731
+    Served sv(s->ctx, n);  // the context's message service, if started (ring_host.hpp)
+    if (sv && (rc = sv.begin(stream))) return rc;
     if (r->compute_size >= totaldata) {  // encryption_common_counter (ring_host.hpp), stream A,
-      rc = ring_encrypt_locked(r, out, in, n, stream);  // under the lock that chose it
+      rc = ring_encrypt_locked(r, out, in, n, stream, sv ? &sv : nullptr);  // under the lock that chose it
       return rc ? rc : 1;
     }
     uint8_t iv[16];
     memcpy(iv, s->ivb, 16);
     cmpi_iv_count(iv, s->enc_common_counter_long_msg);
-    if (n && (rc = ctr_launch(s->ctx, out, in, n, iv, stream))) return rc;
+    if (n && (rc = sv ? sv.ctr(out, in, n, iv) : ctr_launch(s->ctx, out, in, n, iv, stream))) return rc;
     s->enc_common_counter_long_msg += (unsigned long)(totaldata - 1) / 16 + 1;
     s->counter_needto_send_large_msg += ((totaldata - 1) / 16) + 1;
     return 1;
@@ -319,6 +334,9 @@ int cmpi_702_recv_premask(const cmpi_ctx* c, const uint8_t recv_iv[32], const ui
   const uint8_t* ivs = header[4] == '0' ? recv_iv : recv_iv + 16;
   const unsigned long c0 = be32h(header + 5);
   DeviceGuard dg(c->device);
+  Served sv(c, ((size_t)totaldata + 511) / 512 * 512);
+  if (sv)
+    if (int rc = sv.begin(stream)) return rc;
   if (totaldata > 1024) {  // recv.c:1111-1139: 512-byte chunks at IV_Count_out(counter + 32k)
     const size_t need = ((size_t)totaldata + 511) / 512 * 512;
     if (!mask || mask_cap < need) return fail(CMPI_EINVAL, "mask buffer smaller than %zu bytes", need);
@@ -328,7 +346,7 @@ int cmpi_702_recv_premask(const cmpi_ctx* c, const uint8_t recv_iv[32], const ui
       v.push_back({off, 512, ctr});
       ctr += (unsigned long)((512 - 1) / 16 + 1);
     }
-    const int rc = ctr_slices(c, ivs, v, mask, nullptr, stream);
+    const int rc = ctr_slices(c, ivs, v, mask, nullptr, stream, sv ? &sv : nullptr);
     if (rc) return rc;
     *mask_len = need;
     return CMPI_OK;
@@ -338,7 +356,7 @@ int cmpi_702_recv_premask(const cmpi_ctx* c, const uint8_t recv_iv[32], const ui
   uint8_t iv[16];  // recv.c:1187-1194: the whole (<= 1 KiB) mask from IV_Count(iv, counter)
   memcpy(iv, ivs, 16);
   cmpi_iv_count(iv, c0);
-  const int rc = ctr_launch(c, mask, nullptr, (size_t)totaldata, iv, stream);
+  const int rc = sv ? sv.ctr(mask, nullptr, (size_t)totaldata, iv) : ctr_launch(c, mask, nullptr, (size_t)totaldata, iv, stream);
   if (rc) return rc;
   *mask_len = (size_t)totaldata;
   return CMPI_OK;
@@ -356,12 +374,15 @@ int cmpi_702_recv(const cmpi_ctx* c, const uint8_t recv_iv[32], const uint8_t he
   DeviceGuard dg(c->device);
   if (totaldata < kPreCom) {
     const uint8_t* ivs = header[4] == '0' ? recv_iv : recv_iv + 16;
+    Served sv(c, (size_t)totaldata);  // the context's message service, if started (ring_host.hpp)
+    if (sv)
+      if (int rc = sv.begin(stream)) return rc;
     if (mask && mask_len >= (size_t)totaldata)  // decryption_common_counter_ivflag, mask covers it all
-      return xor_launch(out, mask, in, (size_t)totaldata, (hipStream_t)stream);
+      return sv ? sv.xor_(out, mask, in, (size_t)totaldata) : xor_launch(out, mask, in, (size_t)totaldata, (hipStream_t)stream);
     uint8_t iv[16];  // recv.c:1203-1220: no (complete) mask -> direct CTR from the header counter
     memcpy(iv, ivs, 16);
     cmpi_iv_count(iv, c0);
-    return ctr_launch(c, out, in, (size_t)totaldata, iv, stream);
+    return sv ? sv.ctr(out, in, (size_t)totaldata, iv) : ctr_launch(c, out, in, (size_t)totaldata, iv, stream);
   }
   const int chop = (int)be32h(header + 21);
   // a sender's choping_sz is a multiple of 16 in [16, totaldata rounded up to 16] (send.c:1595-1637);

@@ -43,6 +43,36 @@ int ring_ctr(const cmpi_ctr_ring* r, unsigned long counter, uint8_t* out, const 
   return ctr_launch(r->ctx, out, in, n, cb, stream);
 }
 
+// Served counter-mode ops (service_host.hpp): when the context runs a message service
+// (cmpi_service_start on the CTR context), the ring XORs and keystreams of messages up to
+// kSvcMaxStreamLen bytes run on it — one ring post and a completion word instead of a launch and
+// a stream wait.  A served op runs now, not in stream order: begin() waits for the work already
+// queued on the caller's stream (the input's producer), and the ring's last operation is drained
+// before a served ring op (ring_drain).  Holds hmu (after r->mu where a ring is involved).
+struct Served {
+  const cmpi_ctx* c;
+  std::unique_lock<std::mutex> lk;
+  Svc* S = nullptr;
+  Served(const cmpi_ctx* c_, size_t n) : c(c_), lk(c_->hmu) {
+    if (c->svc && n <= cmpi::dev::kSvcMaxStreamLen) S = c->svc;
+    else lk.unlock();
+  }
+  explicit operator bool() const { return S != nullptr; }
+  int begin(void* stream) {
+    const hipError_t e = hipStreamQuery((hipStream_t)stream);
+    if (e == hipSuccess) return CMPI_OK;
+    if (e != hipErrorNotReady) return fail(CMPI_EHIP, "stream: %s", hipGetErrorString(e));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return CMPI_OK;
+  }
+  int xor_(uint8_t* out, const uint8_t* mask, const uint8_t* in, size_t n) {
+    return svc_stream(c, *S, cmpi::dev::kSvcXor, out, in, mask, nullptr, n);
+  }
+  int ctr(uint8_t* out, const uint8_t* in, size_t n, const uint8_t cb[16]) {
+    return svc_stream(c, *S, cmpi::dev::kSvcCtr, out, in, nullptr, cb, n);
+  }
+};
+
 // Ring operations chain on r->last (called with r->mu held): the launch stream waits for the
 // previous operation when it ran on another stream, and records the new last use after.
 struct RingOrder {
@@ -64,6 +94,20 @@ struct RingOrder {
     r->pending = true;
   }
 };
+
+// Before a served ring op: the ring's last stream operation is complete (then nothing is left to
+// order after: the served op completes before the call returns).
+int ring_drain(cmpi_ctr_ring* r) {
+  if (!r->used) return CMPI_OK;
+  if (r->pending) {
+    HIP_TRY(hipStreamSynchronize(r->last_stream));
+  } else {
+    HIP_TRY(hipEventSynchronize(r->last));
+  }
+  r->used = false;
+  r->pending = false;
+  return CMPI_OK;
+}
 
 }  // namespace
 
@@ -167,16 +211,26 @@ int cmpi_ctr_ring_generate(cmpi_ctr_ring* r, size_t gen_bytes, void* stream) {
 
 namespace {
 // send.c:1273-1465, with r->mu held by the caller (cmpi_ctr_ring_encrypt, and cmpi_702_send, whose
-// stream choice and header counter must see the same ring state as the XOR that follows)
-int ring_encrypt_locked(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_t n, void* stream) {
+// stream choice and header counter must see the same ring state as the XOR that follows).
+// sv: the XORs and the keystream tail run on the context's message service (Served, begun).
+int ring_encrypt_locked(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_t n, void* stream,
+                        Served* sv = nullptr) {
   // n == 0 is not a no-op: like the reference, it retires one 16-byte ring block
   // (((0 - 1) / 16) * 16 + 16 == 16, send.c:1331-1335).
   if (n && (!out || !in)) return fail(CMPI_EINVAL, "null buffer");
   if (n > 0x7FFFFFFFu) return fail(CMPI_EINVAL, "message larger than INT_MAX");
   DeviceGuard dg(r->ctx->device);
   hipStream_t st = (hipStream_t)stream;
-  RingOrder ord{r, st};
-  if (int e = ord.begin()) return e;
+  std::optional<RingOrder> ord;
+  if (sv) {
+    if (int e = ring_drain(r)) return e;
+  } else {
+    ord.emplace(RingOrder{r, st});
+    if (int e = ord->begin()) return e;
+  }
+  auto xor_op = [&](uint8_t* o, const uint8_t* m, const uint8_t* i, size_t len) {
+    return sv ? sv->xor_(o, m, i, len) : xor_launch(o, m, i, len, st);
+  };
   const int enc_datasize = (int)n;
   int how_much_generate, temporary_datasize, datasize;
   if (enc_datasize > r->compute_size) {
@@ -190,7 +244,7 @@ int ring_encrypt_locked(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_
   if (r->compute_size > 0) {
     if (r->end > r->start) {
       const int tempamount = (r->start + datasize <= r->end) ? datasize : r->end - r->start;
-      if ((rc = xor_launch(out, r->dring + r->start, in, (size_t)tempamount, st))) return rc;
+      if ((rc = xor_op(out, r->dring + r->start, in, (size_t)tempamount))) return rc;
       r->start += ((tempamount - 1) / 16) * 16 + 16;
       if (r->start >= r->max) r->start = 0;
       r->compute_size -= ((tempamount - 1) / 16) * 16 + 16;
@@ -200,13 +254,13 @@ int ring_encrypt_locked(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_
       int tempnext = 0;
       if (datasize > tempamount) {
         if (tempamount) {
-          if ((rc = xor_launch(out, r->dring + r->start, in, (size_t)tempamount, st))) return rc;
+          if ((rc = xor_op(out, r->dring + r->start, in, (size_t)tempamount))) return rc;
           tempnext = tempamount;
         }
         r->start = 0;
         datasize -= tempamount;
       }
-      if ((rc = xor_launch(out + tempnext, r->dring + r->start, in + tempnext, (size_t)datasize, st))) return rc;
+      if ((rc = xor_op(out + tempnext, r->dring + r->start, in + tempnext, (size_t)datasize))) return rc;
       if (datasize > 0) r->start += ((datasize - 1) / 16) * 16 + 16;
       if (r->start >= r->max) r->start = 0;
       r->compute_size -= ((temporary_datasize - 1) / 16) * 16 + 16;
@@ -214,9 +268,15 @@ int ring_encrypt_locked(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_
     }
   }
   if (how_much_generate) {
-    if ((rc = ring_ctr(r, r->counter, out + temporary_datasize, in + temporary_datasize, (size_t)how_much_generate,
-                       stream)))
-      return rc;
+    if (sv) {
+      uint8_t cb[16];
+      memcpy(cb, r->iv, 16);
+      cmpi_iv_count(cb, r->counter);
+      rc = sv->ctr(out + temporary_datasize, in + temporary_datasize, (size_t)how_much_generate, cb);
+    } else {
+      rc = ring_ctr(r, r->counter, out + temporary_datasize, in + temporary_datasize, (size_t)how_much_generate, stream);
+    }
+    if (rc) return rc;
     r->counter += (unsigned long)((how_much_generate - 1) / 16 + 1);
     r->counter_needto_send += (unsigned long)(((how_much_generate - 1) / 16) + 1);
   }
@@ -229,7 +289,10 @@ extern "C" {
 int cmpi_ctr_ring_encrypt(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_t n, void* stream) {
   if (!r) return fail(CMPI_EINVAL, "null ring");
   std::lock_guard<std::mutex> lk(r->mu);
-  return ring_encrypt_locked(r, out, in, n, stream);
+  Served sv(r->ctx, n);
+  if (sv)
+    if (int e = sv.begin(stream)) return e;
+  return ring_encrypt_locked(r, out, in, n, stream, sv ? &sv : nullptr);
 }
 
 // recv.c:954-1023
@@ -240,12 +303,15 @@ int cmpi_ctr_mask_decrypt(const cmpi_ctx* ctx, uint8_t* out, const uint8_t* in, 
   if (!out || !in || (!mask && mask_len)) return fail(CMPI_EINVAL, "null buffer");
   DeviceGuard dg(ctx->device);
   const size_t len = std::min(n, mask_len);
-  int rc = xor_launch(out, mask, in, len, (hipStream_t)stream);
+  Served sv(ctx, n);
+  if (sv)
+    if (int e = sv.begin(stream)) return e;
+  int rc = sv ? sv.xor_(out, mask, in, len) : xor_launch(out, mask, in, len, (hipStream_t)stream);
   if (rc || n == len) return rc;
   uint8_t cb[16];
   memcpy(cb, iv, 16);
   cmpi_iv_count(cb, (unsigned long)counter);
-  return ctr_launch(ctx, out + len, in + len, n - len, cb, stream);
+  return sv ? sv.ctr(out + len, in + len, n - len, cb) : ctr_launch(ctx, out + len, in + len, n - len, cb, stream);
 }
 
 int cmpi_xor_bytes(uint8_t* out, const uint8_t* a, const uint8_t* b, size_t n, void* stream) {

@@ -2,7 +2,8 @@
 // cmpi_aead.hip.  Opt-in per context (cmpi_service_start): single GCM messages from host memory
 // (cmpi_gcm_seal_host / _open_host with nrec = 1, len <= kSvcMaxLen) are posted to the running
 // service kernel instead of launching the direct path's kernel; the host spins on a page-locked
-// word the kernel writes.  The kernel exits after `idle_us` without messages (the CUs are
+// word the kernel writes.  On CTR contexts the service serves the 702 small-message XORs and
+// keystreams (ctrmode_host.hpp: svc_stream), synchronously and outside stream order.  The kernel exits after `idle_us` without messages (the CUs are
 // returned) and is relaunched by the next message.  No CPU cipher on any path: a service that
 // cannot start fails the call.
 
@@ -16,7 +17,7 @@ constexpr uint64_t kSvcLifeUs = 100000;           // relaunched at least every 1
 
 struct Svc {
   hipStream_t st = nullptr;
-  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..11] (three 16-B chunks), done [32..44]
+  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..15] (four 16-B chunks), done [32..44]
   uint32_t* dw = nullptr;      // its device address
   uint32_t* go = nullptr;      // device control words (64 B), counter (at +64), partials (at +128)
   cmpi::dev::u32x4* wts = nullptr;  // device chunk weights (4 x 64 x 4 blocks)
@@ -31,13 +32,13 @@ struct Svc {
   uint32_t* done() { return hw + 32; }
 };
 
-// Post descriptor d[0..8] under `seq`: chunk c = {seq, d[3c..3c+2]} at ring[4c]; the words first,
-// then seq into every chunk (the kernel takes a chunk's words only with the new seq in all three).
+// Post descriptor d[0..11] under `seq`: chunk c = {seq, d[3c..3c+2]} at ring[4c]; the words first,
+// then seq into every chunk (the kernel takes a chunk's words only with the new seq in all four).
 void svc_post(Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc], uint32_t seq) {
   uint32_t* r = S.ring();
-  for (uint32_t c = 0; c < 3; ++c)
+  for (uint32_t c = 0; c < cmpi::dev::kSvcChunks; ++c)
     for (uint32_t j = 0; j < 3; ++j) r[4 * c + 1 + j] = d[3 * c + j];
-  for (uint32_t c = 0; c < 3; ++c) __atomic_store_n(r + 4 * c, seq, __ATOMIC_RELEASE);
+  for (uint32_t c = 0; c < cmpi::dev::kSvcChunks; ++c) __atomic_store_n(r + 4 * c, seq, __ATOMIC_RELEASE);
 }
 
 constexpr size_t kSvcWtsBytes = 4 * 64 * 4 * 16;
@@ -65,6 +66,10 @@ void svc_release(Svc& S) {
 
 // H^(1 + (63-k)·64·2^s) at wts[256s + 4k + 3] (the flow kernel's chunk-weight slot layout)
 int svc_weights(const cmpi_ctx* c, Svc& S) {
+  if (c->alg != CMPI_AES_128_GCM) {  // counter-mode service: no GHASH
+    S.wts_ok = true;
+    return CMPI_OK;
+  }
   std::vector<Blk> w(4 * 64 * 4);
   for (uint32_t s = 0; s < 4; ++s) {
     const Blk P = cmpi::gf_pow(c->H, 64u << s);
@@ -145,6 +150,39 @@ int svc_shutdown_locked(cmpi_ctx* c) {
   return rc;
 }
 
+// Post descriptor d as the next message (the service launched first if it is not running) and
+// wait for its completion words w (status, tag 0-3).  hmu held.
+int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc], uint32_t (&w)[5]) {
+  if (S.running && svc_exited(S)) {  // idled out since the last message
+    HIP_TRY(hipStreamSynchronize(S.st));
+    S.running = false;
+  }
+  if (!S.running)
+    if (int rc = svc_launch(c, S, S.seq)) return rc;
+  const uint32_t seq = ++S.seq;
+  svc_post(S, d, seq);
+  const auto t0 = std::chrono::steady_clock::now();
+  int relaunches = 0;
+  for (uint32_t i = 1;; ++i) {
+    if (svc_done(S, seq, w)) break;
+    if (svc_exited(S)) {  // the generation ended (lifetime): let every workgroup finish first
+      HIP_TRY(hipStreamSynchronize(S.st));
+      S.running = false;
+      if (svc_done(S, seq, w)) break;
+      if (++relaunches > 2) return fail(CMPI_EHIP, "message service did not complete message %u", seq);
+      if (int rc = svc_launch(c, S, seq - 1)) return rc;  // it never saw the message
+      continue;
+    }
+    if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+      const hipError_t e = hipStreamQuery(S.st);
+      if (e != hipSuccess && e != hipErrorNotReady) return fail(CMPI_EHIP, "service kernel: %s", hipGetErrorString(e));
+      if (e == hipSuccess && !svc_done(S, seq, w) && !svc_exited(S))
+        return fail(CMPI_EHIP, "service kernel ended without completing message %u", seq);
+    }
+  }
+  return CMPI_OK;
+}
+
 // One message through the service.  hmu held; pageable buffers go through the bounce.
 template <bool DEC>
 int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const uint8_t* nonce, size_t len,
@@ -172,12 +210,6 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
     dout = pinned_dev_ptr(hout);
   }
   if (!din || !dout) return fail(CMPI_EHIP, "service buffers have no device address");
-  if (S.running && svc_exited(S)) {  // idled out since the last message
-    HIP_TRY(hipStreamSynchronize(S.st));
-    S.running = false;
-  }
-  if (!S.running)
-    if (int rc = svc_launch(c, S, S.seq)) return rc;
   uint32_t d[cmpi::dev::kSvcDesc] = {DEC ? cmpi::dev::kSvcOpen : cmpi::dev::kSvcSeal,
                                      (uint32_t)len,
                                      (uint32_t)(uintptr_t)din,
@@ -185,28 +217,8 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
                                      (uint32_t)(uintptr_t)dout,
                                      (uint32_t)((uintptr_t)dout >> 32)};
   memcpy(d + 6, nonce, 12);
-  const uint32_t seq = ++S.seq;
-  svc_post(S, d, seq);
-  const auto t0 = std::chrono::steady_clock::now();
-  int relaunches = 0;
   uint32_t w[5];
-  for (uint32_t i = 1;; ++i) {
-    if (svc_done(S, seq, w)) break;
-    if (svc_exited(S)) {  // the generation ended (lifetime): let every workgroup finish first
-      HIP_TRY(hipStreamSynchronize(S.st));
-      S.running = false;
-      if (svc_done(S, seq, w)) break;
-      if (++relaunches > 2) return fail(CMPI_EHIP, "message service did not complete message %u", seq);
-      if (int rc = svc_launch(c, S, seq - 1)) return rc;  // it never saw the message
-      continue;
-    }
-    if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
-      const hipError_t e = hipStreamQuery(S.st);
-      if (e != hipSuccess && e != hipErrorNotReady) return fail(CMPI_EHIP, "service kernel: %s", hipGetErrorString(e));
-      if (e == hipSuccess && !svc_done(S, seq, w) && !svc_exited(S))
-        return fail(CMPI_EHIP, "service kernel ended without completing message %u", seq);
-    }
-  }
+  if (int rc = svc_exec(c, S, d, w)) return rc;
   const int32_t ok = (int32_t)w[0];
   if (hout) memcpy(out, hout, len);
   if (!DEC) memcpy(out + len, w + 1, 16);  // the tag travels in the completion words
@@ -217,13 +229,39 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
   return CMPI_OK;
 }
 
+// One counter-mode op through a CTR context's service (ctrmode_host.hpp, ring_host.hpp): kSvcXor
+// out = in ^ mask, kSvcCtr out = in ^ E_K(ctr + j) (in null: the keystream); device (or page-locked)
+// buffers, len <= kSvcMaxStreamLen.  Synchronous: the bytes are in `out` when it returns.  hmu held.
+int svc_stream(const cmpi_ctx* c, Svc& S, uint32_t op, uint8_t* out, const uint8_t* in, const uint8_t* mask,
+               const uint8_t ctr[16], size_t len) {
+  if (len == 0) return CMPI_OK;
+  if (len > cmpi::dev::kSvcMaxStreamLen) return fail(CMPI_EINVAL, "served counter-mode op over 64 KiB");
+  const uint64_t pi = (uint64_t)(uintptr_t)in, po = (uint64_t)(uintptr_t)out;
+  uint32_t d[cmpi::dev::kSvcDesc] = {op, (uint32_t)len, (uint32_t)pi, (uint32_t)(pi >> 32), (uint32_t)po,
+                                     (uint32_t)(po >> 32)};
+  if (op == cmpi::dev::kSvcXor) {
+    const uint64_t pm = (uint64_t)(uintptr_t)mask;
+    d[6] = (uint32_t)pm;
+    d[7] = (uint32_t)(pm >> 32);
+  } else {
+    const uint64_t h = cmpi::be64(ctr), l = cmpi::be64(ctr + 8);
+    d[8] = (uint32_t)h;
+    d[9] = (uint32_t)(h >> 32);
+    d[10] = (uint32_t)l;
+    d[11] = (uint32_t)(l >> 32);
+  }
+  uint32_t w[5];
+  return svc_exec(c, S, d, w);
+}
+
 }  // namespace
 
 extern "C" {
 
 int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
   if (!c) return fail(CMPI_EINVAL, "null ctx");
-  if (c->alg != CMPI_AES_128_GCM) return fail(CMPI_EINVAL, "the message service serves AES-128-GCM contexts");
+  if (c->alg != CMPI_AES_128_GCM && c->alg != CMPI_AES_128_CTR)
+    return fail(CMPI_EINVAL, "the message service serves AES-128-GCM and AES-128-CTR contexts");
   if (c->dev_keys) return fail(CMPI_EINVAL, "the message service needs a host-keyed context");
   DeviceGuard dg(c->device);
   std::lock_guard<std::mutex> lk(c->hmu);

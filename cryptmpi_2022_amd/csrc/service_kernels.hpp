@@ -33,8 +33,13 @@
 //           three 16-byte system-scope stores: no store waits on another's PCIe acknowledgement,
 //           and the host takes a pair only with the new seq in it, so a pair cannot tear; the host
 //           writes a seal's tag into out + len itself.
+//   counter-mode ops (CTR contexts: the 702 / 700 small-message XORs, send.c:1273-1465,
+//           recv.c:954-1023, :1187-1220): kSvcXor out = in ^ mask, kSvcCtr out = in ^ E_K(ctr + j)
+//           (in null: the keystream), at most kSvcMaxStreamLen bytes, served by the leader's
+//           workgroup alone and completed like a seal (status 1, no tag).
 // Every wave's wait loop is bounded by the wall clock: the grid drains even if the host vanishes.
 #pragma once
+#include "ctr_kernels.hpp"
 #include "gcm_kernels.hpp"
 
 namespace cmpi {
@@ -43,13 +48,17 @@ namespace dev {
 constexpr uint32_t kSvcThreads = 512u;
 constexpr uint32_t kSvcGroups = 8u;      // workgroups (one per XCD when the chip is free)
 constexpr uint32_t kSvcMaxChunks = 64u;  // kSvcGroups x 8 waves
-constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u;
-constexpr uint32_t kSvcDesc = 9u;  // descriptor words: op, len, in lo/hi, out lo/hi, nonce[3]
+constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u, kSvcXor = 3u, kSvcCtr = 4u;
+// descriptor words: op, len, in lo/hi, out lo/hi, then the op's own: GCM nonce[3] at 6..8, XOR
+// mask lo/hi at 6..7, CTR counter block as big-endian halves hi lo/hi, lo lo/hi at 8..11
+constexpr uint32_t kSvcDesc = 12u;
+constexpr uint32_t kSvcChunks = kSvcDesc / 3u;  // ring chunks {seq, three descriptor words}
+constexpr uint32_t kSvcMaxStreamLen = 65536u;   // counter-mode ops: the 702 ring's small messages
 
 struct SvcArgs {
   const uint32_t* ring;  // page-locked host words (device address): chunks [4c] = seq, [4c+1..4c+3] = desc[3c..3c+2]
   uint32_t* done;        // page-locked host words: [0..9] five {seq, word} pairs (status, tag 0-3), [12] exited generation
-  uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [3] seqlock version, [4..12] descriptor copy
+  uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [3] seqlock version, [4..15] descriptor copy
   uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
   u32x4* part;           // device: one partial per workgroup
   const u32x4* wts;      // device: 4 x 64 x 4; wts[256s + 4k + 3] = H^(1 + (63-k)·64·2^s)
@@ -94,7 +103,7 @@ __device__ __forceinline__ u32x4 wt_load16(const u32x4* p) {
 }
 
 // LDS words shared by the workgroup (inside the flow aggregation area)
-constexpr uint32_t kSvcX = kFlowAgg + 256u;  // [0] exit, [1] seq, [2..10] descriptor, [11] last, [12] ok
+constexpr uint32_t kSvcX = kFlowAgg + 256u;  // [0] exit, [1] seq, [2..13] descriptor, [14] last, [15] ok
 constexpr uint32_t kSvcTag = kFlowAgg + 128u;  // the XOR of the partials (16 B)
 
 // A 64-bit address from two LDS words (lo, hi), wave-uniform.  readfirstlane returns int: each
@@ -167,11 +176,11 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
         for (uint32_t j = 1; j < ngrp; ++j) x ^= wt_load16(s.part + j);
       }
     }
-    lds_st32(kSvcX + 44u, last);
+    lds_st32(kSvcX + 56u, last);
     lds_st128(kSvcTag, x);
   }
   __syncthreads();
-  if (!lds32(kSvcX + 44u)) return;  // workgroup-uniform
+  if (!lds32(kSvcX + 56u)) return;  // workgroup-uniform
   // the last arriver: tag / verdict, then the host word
   if (threadIdx.x == 0u) {
     uint32_t ok = 1u;
@@ -179,10 +188,10 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
       const u32x4 d = ld_blk(inp + len) ^ lds128(kSvcTag);
       ok = (d[0] | d[1] | d[2] | d[3]) == 0u ? 1u : 0u;
     }
-    lds_st32(kSvcX + 48u, ok);
+    lds_st32(kSvcX + 60u, ok);
   }
   __syncthreads();
-  if (DECRYPT && !lds32(kSvcX + 48u)) {  // forged: zero-fill the plaintext (after every workgroup's stores)
+  if (DECRYPT && !lds32(kSvcX + 60u)) {  // forged: zero-fill the plaintext (after every workgroup's stores)
     const uint32_t full4 = len & ~3u;
     for (uint32_t i = threadIdx.x * 4u; i < full4; i += kSvcThreads * 4u) *reinterpret_cast<u32a*>(outp + i) = 0u;
     for (uint32_t i = full4 + threadIdx.x; i < len; i += kSvcThreads) outp[i] = 0u;
@@ -193,9 +202,45 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
     if (ngrp > 1u) wt_store(s.cnt, 0u);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the record bytes (every wave waited for its own) reach the host first
     const u32x4 tag = DECRYPT ? u32x4{0u, 0u, 0u, 0u} : lds128(kSvcTag);
-    sys_store16(s.done, u32x4{seq, lds32(kSvcX + 48u), seq, tag[0]});
+    sys_store16(s.done, u32x4{seq, lds32(kSvcX + 60u), seq, tag[0]});
     sys_store16(s.done + 4, u32x4{seq, tag[1], seq, tag[2]});
     sys_store16(s.done + 8, u32x4{seq, tag[3], 0u, 0u});
+  }
+}
+
+// Counter-mode op (leader workgroup): 16 bytes per lane and step, the last block's bytes only;
+// kSvcCtr counts blocks like ctr_kernel (a 128-bit big-endian increment).  Every wave waits for
+// its stores, then one system-scope release (the output reaches memory before the completion).
+__device__ __forceinline__ void svc_stream_op(const SvcArgs& s, const RowLanes& rl, uint32_t op, uint32_t seq) {
+  const uint32_t len = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 12u));
+  const uint8_t* inp = reinterpret_cast<const uint8_t*>(lds_ptr64(kSvcX + 16u));
+  uint8_t* outp = reinterpret_cast<uint8_t*>(lds_ptr64(kSvcX + 24u));
+  const uint8_t* mask = reinterpret_cast<const uint8_t*>(lds_ptr64(kSvcX + 32u));
+  const uint64_t chi = lds_ptr64(kSvcX + 40u), clo = lds_ptr64(kSvcX + 48u);
+  const uint32_t nblk = (len + 15u) >> 4;
+  for (uint32_t j = threadIdx.x; j < nblk; j += kSvcThreads) {
+    const uint32_t off = 16u * j, rem = len - off < 16u ? len - off : 16u;
+    u32x4 ks;
+    if (op == kSvcXor) {
+      ks = rem == 16u ? ld_blk(mask + off) : load_partial(mask + off, rem);
+    } else {
+      uint32_t w0, w1, w2, w3;
+      ctr_words(chi, clo, j, w0, w1, w2, w3);
+      aes128_enc(s.rk, rl, w0, w1, w2, w3);
+      ks = u32x4{w0, w1, w2, w3};
+    }
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (inp) v = rem == 16u ? ld_blk(inp + off) : load_partial(inp + off, rem);
+    if (rem == 16u) st_blk(outp + off, v ^ ks);
+    else store_partial(outp + off, v ^ ks, rem);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    sys_store16(s.done, u32x4{seq, 1u, seq, 0u});
+    sys_store16(s.done + 4, u32x4{seq, 0u, seq, 0u});
+    sys_store16(s.done + 8, u32x4{seq, 0u, 0u, 0u});
   }
 }
 
@@ -226,14 +271,16 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
       if (leader) {
         for (;;) {
           asm volatile("" ::: "memory");  // a fresh read every pass
-          u32x4 c0 = sys_load16(s.ring), c1 = sys_load16(s.ring + 4), c2 = sys_load16(s.ring + 8);
-          asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2));  // all three reads in flight together
+          u32x4 c0 = sys_load16(s.ring), c1 = sys_load16(s.ring + 4), c2 = sys_load16(s.ring + 8),
+                c3 = sys_load16(s.ring + 12);
+          asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));  // all four reads in flight together
           q = c0[0];
           if (q != cur) {
-            if (c1[0] != q || c2[0] != q) continue;  // the host is between chunks: read again
+            if (c1[0] != q || c2[0] != q || c3[0] != q) continue;  // the host is between chunks: read again
             d[0] = c0[1], d[1] = c0[2], d[2] = c0[3];
             d[3] = c1[1], d[4] = c1[2], d[5] = c1[3];
             d[6] = c2[1], d[7] = c2[2], d[8] = c2[3];
+            d[9] = c3[1], d[10] = c3[2], d[11] = c3[3];
             if (d[0] == kSvcStop) ex = 1u;
             break;
           }
@@ -245,7 +292,7 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
           __builtin_amdgcn_s_sleep(2);
         }
         uint32_t ls_, nch_;
-        if (!ex && svc_plan(d[1], ls_, nch_) > 1u) {  // seqlock: version odd while the descriptor is rewritten
+        if (!ex && d[0] <= kSvcOpen && svc_plan(d[1], ls_, nch_) > 1u) {  // seqlock: version odd while the descriptor is rewritten
           wt_store(s.go + 3, ++ver);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -297,7 +344,8 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
     const uint32_t q = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 4u));
     const uint32_t op = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 8u));
     if (op == kSvcOpen) svc_message<true>(s, rl, q);
-    else svc_message<false>(s, rl, q);
+    else if (op == kSvcSeal) svc_message<false>(s, rl, q);
+    else if (leader) svc_stream_op(s, rl, op, q);  // counter-mode ops are never published
     __syncthreads();  // LDS words reused by the next message
     cur = q;
     t_last = wall_clock64();

@@ -19,6 +19,9 @@
  * Data pointers are device memory, headers and IVs host memory.  Calls on one sender (send,
  * precompute) may come from several threads: the ring lock is held from the stream choice of a
  * send to the XOR that consumes the ring; they are stream-ordered among themselves.
+ * With a message service started on the CTR context (cmpi_service.h), the ops of messages up to
+ * 64 KiB (ring XOR, direct CTR, premask, mask XOR) run on the resident kernel: the call waits
+ * for the work already queued on `stream`, and returns with its output written.
  */
 #ifndef CMPI_CTRMODE_H
 #define CMPI_CTRMODE_H

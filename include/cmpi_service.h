@@ -21,7 +21,14 @@
  * other greatest-priority streams of the process and more than GPU_MAX_HW_QUEUES concurrently
  * running services may.  hipDeviceSynchronize / torch.cuda.synchronize() wait for the kernel to
  * exit: call cmpi_service_stop first, or keep idle_us short.
- * Host-keyed AES-128-GCM contexts only (CMPI_EINVAL otherwise).  cmpi_ctx_rekey and
+ * On an AES-128-CTR context the service serves CryptMPI's counter-mode small messages instead
+ * (cmpi_ctrmode.h, cmpi_ring.h: the 702 ring XOR, send.c:1273-1465; the receiver's premask and
+ * mask XOR, recv.c:954-1023, :1107-1220; the 700 / 702 direct CTR of messages up to 64 KiB):
+ * each such op of at most 64 KiB is posted to the kernel instead of launched, and is complete
+ * when the call returns.  It runs outside stream order, so the call first waits for the work
+ * already queued on its `stream` (and for the ring's last fill); bytes, headers and ring state
+ * are those of the launched form.
+ * Host-keyed AES-128-GCM and AES-128-CTR contexts only (CMPI_EINVAL otherwise).  cmpi_ctx_rekey and
  * cmpi_ctx_rekey_subkey stop a running service (the next message restarts it with the new key;
  * a device-keyed context ends the service).  cmpi_ctx_free stops it.
  */

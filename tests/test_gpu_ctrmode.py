@@ -3,7 +3,10 @@
 pre-computed counter (send.c:1502-1987 / recv.c:1025-1403) — 26-byte headers, ciphertext, the
 sender's ring / counter state after every call, the receiver's in-flight mask and its direct
 path, over message sequences that cross every branch (ring hit '0', stream B '1', mode '4',
-pipelined '1' > 1 MiB, ring wrap with small rings, multithreaded generation, empty messages)."""
+pipelined '1' > 1 MiB, ring wrap with small rings, multithreaded generation, empty messages).
+Every test runs twice: with a launch per op, and with the context's message service started
+(`served`: the ring XORs and keystreams of messages up to 64 KiB run on the resident kernel,
+ring_host.hpp Served)."""
 import random
 
 import pytest
@@ -20,6 +23,16 @@ KEY = bytes(range(16))
 IV32 = splitmix64_bytes(0x702, 32).tobytes()
 
 
+@pytest.fixture(params=[False, True], ids=["launch", "served"])
+def ctx(request):
+    c = aead.CipherCtx(KEY, "aes-128-ctr")
+    if request.param:
+        c.service_start()
+    yield c
+    if request.param:
+        c.service_stop()
+
+
 def _seq(seed: int):
     rng = random.Random(seed)
     sizes = [0, 1, 15, 16, 17, 1000, 1024, 1025, 3000, 4095, 4096, 65535, 65536, 65537, 300000, 1048575,
@@ -30,8 +43,7 @@ def _seq(seed: int):
 
 
 @pytest.mark.parametrize("ring_bytes,series,seed", [(8 << 20, 16, 1), (65536, 4, 2), (20480, 1, 3)])
-def test_702_sender_sequence_vs_oracle(ring_bytes, series, seed):
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
+def test_702_sender_sequence_vs_oracle(ring_bytes, series, seed, ctx):
     s = ctrmode.Sender702(ctx, IV32, ring_bytes=ring_bytes, series_threads=series)
     o = oracle.Sender702(KEY, IV32, max_bytes=ring_bytes, series=series)
     assert s.state() == o.state()
@@ -50,10 +62,9 @@ def test_702_sender_sequence_vs_oracle(ring_bytes, series, seed):
 
 
 @pytest.mark.parametrize("n", [0, 1, 16, 17, 1000, 1024, 1025, 4096, 5000, 65535, 65536, 100001, 1048576, (1 << 21) + 7])
-def test_702_receiver_premask_and_direct(n):
+def test_702_receiver_premask_and_direct(n, ctx):
     """recv.c:1107-1220: the mask made while the payload is in flight, then XOR; or the direct
     path when the payload arrived first — both equal the oracle and round-trip the sender."""
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
     s = ctrmode.Sender702(ctx, IV32)
     o = oracle.Sender702(KEY, IV32)
     # push the sender into stream B for some sizes: a message bigger than the ring holds
@@ -78,10 +89,9 @@ def test_702_receiver_premask_and_direct(n):
 
 
 @pytest.mark.parametrize("n", [1, 17, 100, 1000])
-def test_702_premask_writes_only_its_bytes(n):
+def test_702_premask_writes_only_its_bytes(n, ctx):
     """A <= 1 KiB mask of a length that is not a multiple of 16 (recv.c:1187-1194): the keystream
     kernel stores the last block's bytes only — nothing past mask_len changes."""
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
     s = ctrmode.Sender702(ctx, IV32)
     pt = splitmix64_bytes(n + 11, n)
     ct = empty(n)
@@ -97,11 +107,10 @@ def test_702_premask_writes_only_its_bytes(n):
 
 
 @pytest.mark.parametrize("n,mode", [(200000, b"4"), (3000, b"0"), (40000, b"1"), (3 << 20, b"1")])
-def test_702_iv_count_carry_breaks_runs(n, mode):
+def test_702_iv_count_carry_breaks_runs(n, mode, ctx):
     """Header counters near 2^32 and IVs ending in 0xff: IV_Count's 32-bit accumulator
     (send.c:1021) truncates the counter and drops a carry between the reference's slices / mask
     chunks, so they are NOT one CTR stream — the engine must split its launches exactly there."""
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
     iv = IV32[:15] + b"\xff" + IV32[16:31] + b"\xff"
     hdr = bytearray(26)
     hdr[0:4] = n.to_bytes(4, "big")
@@ -120,8 +129,7 @@ def test_702_iv_count_carry_breaks_runs(n, mode):
         assert host(out)[:n].tobytes() == oracle.recv702(KEY, iv, hdr, ct.tobytes(), premask=use_mask), use_mask
 
 
-def test_700_sequence_vs_oracle():
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
+def test_700_sequence_vs_oracle(ctx):
     iv = IV32[:16]
     c = oc = 5
     for n in [1, 15, 16, 17, 4096, 65536, 100000, 1 << 20, (1 << 21) + 3]:
@@ -136,13 +144,12 @@ def test_700_sequence_vs_oracle():
     torch.cuda.synchronize()
 
 
-def test_recv_refuses_untrusted_header_sizes():
+def test_recv_refuses_untrusted_header_sizes(ctx):
     """The header is wire input: a length beyond the caller's buffer, or a choping_sz
     that is not a multiple of 16 in [16, n rounded up to 16], is refused before any launch or
     slice list is built (the reference trusts both, recv.c:1226-1240)."""
     from cryptmpi_2022_amd import _native as N
 
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
     n = 200000
     ct = empty(n)
     out = empty(n - 1)  # one byte short
@@ -162,3 +169,24 @@ def test_recv_refuses_untrusted_header_sizes():
     hdr[21:25] = (16704).to_bytes(4, "big")
     ctrmode.recv702(ctx, IV32, bytes(hdr), out, ct)  # a well-formed header still opens
     assert host(out)[:n].tobytes() == oracle.recv702(KEY, IV32, bytes(hdr), host(ct)[:n].tobytes(), premask=False)
+
+
+def test_served_ops_follow_the_stream(ctx):
+    """A served op runs outside stream order, so it must first wait for the work already queued
+    on the caller's stream: the input is written by a copy queued behind a long sleep kernel, the
+    send / receive right after must see the final bytes (both forms)."""
+    n = 4096
+    s = ctrmode.Sender702(ctx, IV32)
+    pt = splitmix64_bytes(0x5E, n)
+    src = dev(pt)
+    inp = empty(n, fill=0)
+    torch.cuda._sleep(20_000_000)  # ~10 ms of GPU time ahead of the copy
+    inp.copy_(src)
+    ct = empty(n)
+    hdr, _ = s.send(ct, inp, n)
+    out = empty(n, fill=0)
+    torch.cuda._sleep(20_000_000)
+    ct2 = ct.clone()
+    ctrmode.recv702(ctx, IV32, hdr, out, ct2)
+    assert host(out).tobytes() == pt.tobytes()
+    s.close()

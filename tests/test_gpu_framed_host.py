@@ -93,9 +93,19 @@ def test_602_host_pipelined_send_and_receive(n, threads, pinned):
         assert not out2[start:].any() and out2[:start].tobytes() == pt[:start].tobytes()
 
 
-@pytest.mark.parametrize("pinned", [False, True])
-def test_700_host_sequence(pinned):
+def _ctr_ctx(served: bool):
+    """CTR context; served: its message service started (the 700 / 702 ops up to 64 KiB run on
+    the resident kernel, synchronously inside *_begin)."""
     ctx = aead.CipherCtx(KEY, "aes-128-ctr")
+    if served:
+        ctx.service_start()
+    return ctx
+
+
+@pytest.mark.parametrize("served", [False, True])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_700_host_sequence(pinned, served):
+    ctx = _ctr_ctx(served)
     iv = IV32[:16]
     c = oc = 9
     for n in [0, 1, 17, 4096, 65536, 100001, (1 << 21) + 3]:
@@ -111,13 +121,14 @@ def test_700_host_sequence(pinned):
         assert back.tobytes() == pt.tobytes(), n
 
 
+@pytest.mark.parametrize("served", [False, True])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_702_host_sequence_vs_oracle(pinned):
+def test_702_host_sequence_vs_oracle(pinned, served):
     """702 sender from host buffers over the branch mix (ring hit '0', stream B '1', mode '4',
     pipelined '1'), interleaved with the precompute a sender runs while its Isends are pending;
     every header, ciphertext and sender state equal to the oracle's; the receiver's host form
     with the device mask made while the payload is in flight, and without a mask."""
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
+    ctx = _ctr_ctx(served)
     s = ctrmode.Sender702(ctx, IV32, ring_bytes=65536, series_threads=8)
     o = oracle.Sender702(KEY, IV32, max_bytes=65536, series=8)
     for i, n in enumerate([0, 16, 1000, 4096, 30000, 65535, 65536, 200000, 1048576, (1 << 21) + 9, 3000, 70000]):

@@ -17,12 +17,23 @@ pytestmark = pytest.mark.gpu
 KEY = bytes(range(16))
 
 
+@pytest.fixture(params=[False, True], ids=["launch", "served"])
+def ctx(request):
+    """CTR context; served: its message service started (ring XORs / keystreams up to 64 KiB
+    run on the resident kernel, ring_host.hpp Served)."""
+    c = aead.CipherCtx(KEY, "aes-128-ctr")
+    if request.param:
+        c.service_start()
+    yield c
+    if request.param:
+        c.service_stop()
+
+
 @pytest.mark.parametrize("ring_bytes,seed", [(4096, 1), (8192, 2), (65536, 3), (8 << 20, 4)])
-def test_ring_matches_oracle(ring_bytes, seed):
+def test_ring_matches_oracle(ring_bytes, seed, ctx):
     iv = splitmix64_bytes(0x1A + seed, 16).tobytes()
     if seed == 2:
         iv = bytes(12) + b"\xff\xff\xff\xf0"  # counter blocks carry through the 32-bit tail
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
     g = ring.CtrRing(ctx, iv, ring_bytes)
     o = oracle.Ring(KEY, iv, ring_bytes)
     rnd = random.Random(seed)
@@ -54,21 +65,19 @@ def test_ring_matches_oracle(ring_bytes, seed):
 
 
 @pytest.mark.parametrize("n,mask_len,counter", [(100, 40, 0), (5000, 4096, 7), (4096, 8192, 3), (33, 0, 2**32 - 1)])
-def test_mask_decrypt_matches_oracle(n, mask_len, counter):
+def test_mask_decrypt_matches_oracle(n, mask_len, counter, ctx):
     iv = splitmix64_bytes(0x77 + n, 16).tobytes()
     mask = splitmix64_bytes(0x78 + n, mask_len)
     ct = splitmix64_bytes(0x79 + n, n)
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
     out = empty(n)
     ring.mask_decrypt(ctx, out, dev(ct), n, dev(mask) if mask_len else None, mask_len, iv, counter)
     assert host(out)[:n].tobytes() == oracle.mask_decrypt(KEY, iv, counter, mask.tobytes(), ct.tobytes())
 
 
-def test_sender_ring_receiver_mask_round_trip():
+def test_sender_ring_receiver_mask_round_trip(ctx):
     """A sender encrypting through its ring and a receiver holding the same keystream as its
     precomputed dec mask recover the plaintext (the 702 pairing of send.c / recv.c)."""
     iv = bytes(range(32, 48))
-    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
     g = ring.CtrRing(ctx, iv, 1 << 16)
     assert g.generate(10000) == 1
     n = 30000
