@@ -1106,6 +1106,9 @@ def ctr702_rates(device: int, steps: int = 50) -> dict:
                        "GiBps": round(n / dt / GIB, 2), "verified": bool(torch.equal(back, pt))}
     s.close()
     ctx.close()
+    res["note"] = ("timed from Python: five ctypes calls per message (send, precompute, premask, receive) "
+                   "bound the 4 KiB rate; the C-timed per-op latencies, launched and served, are in "
+                   "extras.c_timed_latency")
     return res
 
 
