@@ -1221,7 +1221,8 @@ def seal_kernel_name(w) -> str:
     L, nseg, _, _ = aead.gcm_plan(w.ctx, w.n, w.nrec)
     if L == 64:
         return "gcm_flow_kernel<false,...>" + (" + gcm_xor_combine_kernel<false>" if nseg > 1 else "")
-    return f"gcm_lane_kernel<{L}, false>" + (" + gcm_combine_kernel<false>" if nseg > 1 else "")
+    # third template argument: the record-store form (2 = line-aligned stores, the default at L = 4)
+    return f"gcm_lane_kernel<{L}, false, {2 if L == 4 else 0}>" + (" + gcm_combine_kernel<false>" if nseg > 1 else "")
 
 
 def spawn_ranks(n: int) -> None:

@@ -212,7 +212,11 @@ __device__ __forceinline__ void build_byte_table(const u32x4* __restrict__ src, 
 // Lane groups (many records): see the file header.  Waves take wave priority by progress
 // (progress_prio: a workgroup counter in LDS; behind the average -> priority 3), so waves of
 // equal work finish together.
-template <int L, bool DECRYPT>
+// PAIR (L = 4): the record stores are grouped by 128-byte output line — a group's lanes hold their
+// outputs of the last two steps and store a line's 8 blocks together in the step that completes
+// it, so each line reaches the L2 whole instead of as two halves a step apart; the computation's
+// schedule is unchanged.
+template <int L, bool DECRYPT, int PAIR>
 __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
   CMPI_PROBE(a, 0u);
   stage_rows(a.te0, kGcmRows);
@@ -273,13 +277,61 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
     uint8_t* op = out_rec + 16u * x0;
     if (nfull > 0u) {
       auto ld = [&](uint32_t uu) { return ld_blk(ip + 16u * (uu < nfull ? uu : nfull - 1u)); };
-      u32x4 v = ld(q);
-      for (uint32_t u = q; u < nfull; u += (uint32_t)L) {
-        progress_prio(gcm_prog_off(L), ++done);
-        const u32x4 o = v ^ keystream(2u + x0 + u);
-        st_blk(op + 16u * u, o);
-        acc = gmul_byte(acc, gl, DECRYPT ? v : o);
-        v = ld(u + (uint32_t)L);
+      if constexpr (PAIR != 0 && L == 4) {
+        // Line-aligned stores: a 128-byte line of the output holds 8 blocks, two group steps.  The
+        // group's blocks are computed in order as always; each lane keeps its outputs of the last
+        // two steps (h1, h2) and the lanes store a line's 8 blocks together in the step that
+        // completes it (every other step), so each line reaches the L2 whole.  s0 = position of
+        // block 0 in its line (16-byte units, absolute address); steps run for all four lanes.
+        const int32_t s0 = (int32_t)(((uint64_t)(uintptr_t)op >> 4) & 7u);
+        const int32_t nf = (int32_t)nfull;
+        const uint32_t nsteps = (nfull + 3u) >> 2;
+        u32x4 v = ld(q), h1 = {0u, 0u, 0u, 0u}, h2 = {0u, 0u, 0u, 0u};
+        auto put = [&](int32_t b, u32x4 x) {
+          if (b >= 0 && b < nf) st_blk(op + 16u * (uint32_t)b, x);
+        };
+        for (uint32_t k = 0; k < nsteps; ++k) {
+          const int32_t u = 4 * (int32_t)k + (int32_t)q;
+          progress_prio(gcm_prog_off(L), ++done);
+          const u32x4 o = v ^ keystream(2u + x0 + (uint32_t)u);
+          const int32_t j = (s0 + 4 * (int32_t)k) & 7;
+          if constexpr (PAIR == 1) {
+            if (j >= 4) {  // this step ends the line of blocks [4k - j, 4k + 7 - j]
+              if ((int32_t)q + j <= 7) {
+                put(u - 4, h1);
+                put(u, o);
+              } else {
+                put(u - 8, h2);
+                put(u - 4, h1);
+              }
+            }
+          } else {  // the same stores as selects: two predicated stores per step, no branches
+            const bool cur = (int32_t)q + j <= 7;
+            const int32_t ba = cur ? u - 4 : u - 8;
+            const u32x4 xa = cur ? h1 : h2, xb = cur ? o : h1;
+            if (j >= 4 && ba >= 0) st_blk(op + 16u * (uint32_t)ba, xa);
+            if (j >= 4 && ba + 4 >= 0 && ba + 4 < nf) st_blk(op + 16u * (uint32_t)(ba + 4), xb);
+          }
+          h2 = h1;
+          h1 = o;
+          if (u < nf) acc = gmul_byte(acc, gl, DECRYPT ? v : o);
+          v = ld((uint32_t)u + 4u);
+        }
+        // the blocks after the last completed line
+        const int32_t kl = (int32_t)nsteps - 1, jl = (s0 + 4 * kl) & 7;
+        const int32_t F = jl >= 4 ? 4 * kl + 7 - jl : 4 * kl - 1 - jl;
+        const int32_t b1 = 4 * kl + (int32_t)q, b2 = b1 - 4;
+        if (b2 > F) put(b2, h2);
+        if (b1 > F) put(b1, h1);
+      } else {
+        u32x4 v = ld(q);
+        for (uint32_t u = q; u < nfull; u += (uint32_t)L) {
+          progress_prio(gcm_prog_off(L), ++done);
+          const u32x4 o = v ^ keystream(2u + x0 + u);
+          st_blk(op + 16u * u, o);
+          acc = gmul_byte(acc, gl, DECRYPT ? v : o);
+          v = ld(u + (uint32_t)L);
+        }
       }
     }
     // ---- special slots: partial last block, length block, J0 (the lane's slots >= nfull)

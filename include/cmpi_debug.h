@@ -37,6 +37,10 @@ void cmpi_debug_event_free(void* ev);
 /* gcm_flow_kernel threads per workgroup: 0 automatic (512 when the batch is at most 8 waves per
  * CU, else 1024), 512 or 1024 forced (the chunk plan then assumes that many waves per CU). */
 void cmpi_debug_set_flow_threads(int threads);
+/* gcm_lane_kernel (L = 4) record stores grouped by 128-byte output line (each line stored whole in
+ * the step that completes it): 2 = predicated selects (default), 1 = branches, 0 = a store per
+ * step. */
+void cmpi_debug_set_lane_pair(int on);
 /* FLOW kernel: a batch whose chunks all fit one workgroup finishes its tags in-kernel (1, default)
  * or through the XOR-combine launch (0). */
 void cmpi_debug_set_flow_one_wg(int on);

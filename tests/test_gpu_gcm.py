@@ -31,6 +31,7 @@ def _auto_plan():
     aead.set_flow_threads(0)
     aead.set_flow_one_wg(True)
     aead.N.lib().cmpi_debug_set_host_direct(DIRECT_DEFAULT)
+    aead.N.lib().cmpi_debug_set_lane_pair(2)  # the default
 
 
 def gpu_seal(ctx, nonces: np.ndarray, pt: np.ndarray) -> np.ndarray:
@@ -78,10 +79,14 @@ def test_openssl_vectors(golden):
         assert st[0] == 1 and back[0].tobytes() == pt[0].tobytes()
 
 
+@pytest.mark.parametrize("pair", [0, 1, 2])
 @pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 31, 48, 100, 1024, 1040, 4096, 4097, 65535])
 @pytest.mark.parametrize("plan", [(0, 0), (1, 1), (2, 1), (4, 1), (4, 3), (1, 2), (2, 7)])
-def test_batch_parity_plans(n, plan):
+def test_batch_parity_plans(n, plan, pair):
+    """Every lane plan, with the lane kernel's main loop one slot or two slots per iteration
+    (cmpi_debug_set_lane_pair)."""
     aead.force_plan(*plan)
+    aead.N.lib().cmpi_debug_set_lane_pair(pair)
     nrec = 24 if n <= 4096 else 4
     pt = records(0x1000 + n, nrec, n)
     nonces = random_nonces(0x2000 + n, nrec)

@@ -3,7 +3,7 @@
 single 64 KiB messages, 3 x 100000 B, 1 x 8 MiB, 32 x 256 KiB) and two ragged ones (8 x (1 MiB - 5),
 65536 x 1000 B on the lane kernel) and short records (1000 B, 100 B; few of them).
 
-    python tools/flow_ab.py <libA.so> <libB.so> [rounds]
+    [AB_SHAPES=65536x1024,65536x4096] python tools/flow_ab.py <libA.so> <libB.so> [rounds]
     (a build may carry test hooks: path/libcmpi_aead.so@lane_aligned=0 calls
      cmpi_debug_set_lane_aligned(0) in that build's processes)
 
@@ -25,6 +25,12 @@ SHAPES = {"8x1MiB": (1 << 20, 8), "1x64KiB": (65536, 1), "3x100000": (100000, 3)
           "256x260": (260, 256), "16x300": (300, 16), "65536x1024": (1024, 65536), "65536x4096": (4096, 65536)}
 
 
+def shapes() -> dict:
+    """SHAPES, or the comma-separated subset named by AB_SHAPES."""
+    sel = [x for x in os.environ.get("AB_SHAPES", "").split(",") if x]
+    return {k: v for k, v in SHAPES.items() if not sel or k in sel}
+
+
 def child() -> None:
     sys.path.insert(0, ROOT)
     import torch
@@ -37,7 +43,7 @@ def child() -> None:
         getattr(N.lib(), "cmpi_debug_set_" + k)(int(v))
 
     out = {}
-    for name, (n, nrec) in SHAPES.items():
+    for name, (n, nrec) in shapes().items():
         bench.WORKLOADS["_ab"] = ("gcm", n, nrec, name)
         w = bench.Workload("_ab", 0, seed=5)
         st = torch.cuda.current_stream().cuda_stream
@@ -84,7 +90,7 @@ def main() -> None:
                 sys.exit(p.returncode)
             runs[lib].append(json.loads(p.stdout.strip().splitlines()[-1]))
     res = {}
-    for name in SHAPES:
+    for name in shapes():
         row = {}
         for lib in libs:
             s = sorted(r[name]["seal_us"] for r in runs[lib])

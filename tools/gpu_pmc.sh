@@ -2,7 +2,7 @@
 # PMC passes (one counter group per pass, --kernel-trace only, never with sys/runtime traces).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-out=gpurun_out/pmc_${WL:-gcm1k}
+out=${PMC_OUT:-gpurun_out/pmc_${WL:-gcm1k}}
 mkdir -p "$out"
 export TMPDIR=/tmp
 WL=${WL:-gcm1k}
