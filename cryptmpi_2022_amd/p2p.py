@@ -35,7 +35,9 @@ class Endpoint:
         self.hdr_in = torch.zeros(HEADER, dtype=torch.uint8)
 
     def send(self, msg: np.ndarray, dst: int, group=None, nonce: bytes | None = None) -> None:
-        """send.c:221-337: header, then nonce || seal(msg) from pinned staging."""
+        """send.c:221-337: the header goes out first (MPI_Isend_original, :288) and travels while
+        the message is sealed into pinned staging, then nonce || ct || tag (:330), both waited
+        (:333-334)."""
         import torch
         import torch.distributed as dist
 
@@ -46,14 +48,17 @@ class Endpoint:
         hb = (ctypes.c_uint8 * HEADER)()
         N.check(L.cmpi_600_header(n, ord("1"), hb))
         self.hdr_out.numpy()[:] = np.frombuffer(bytes(hb), np.uint8)
+        w_hdr = dist.isend(self.hdr_out, dst, group=group)
         sb = self.send_buf.numpy()
         sb[:12] = np.frombuffer(nonce if nonce is not None else os.urandom(12), np.uint8)  # RAND_bytes
         src = np.ascontiguousarray(msg).reshape(-1).view(np.uint8)  # sealed where it lies (MPI user buffer)
         base = self.send_buf.data_ptr()
-        N.check(L.cmpi_gcm_seal_host(self.ctx.handle, ctypes.c_void_p(base + 12), n + 16,
-                                     ctypes.c_void_p(src.ctypes.data if n else base), max(n, 1),
-                                     ctypes.c_void_p(base), 12, n, 1))
-        dist.send(self.hdr_out, dst, group=group)
+        try:
+            N.check(L.cmpi_gcm_seal_host(self.ctx.handle, ctypes.c_void_p(base + 12), n + 16,
+                                         ctypes.c_void_p(src.ctypes.data if n else base), max(n, 1),
+                                         ctypes.c_void_p(base), 12, n, 1))
+        finally:
+            w_hdr.wait()  # the header buffer is reused by the next message
         dist.send(self.send_buf[: n + OVERHEAD], dst, group=group)
 
     def recv(self, src: int, group=None, out: np.ndarray | None = None) -> np.ndarray:
