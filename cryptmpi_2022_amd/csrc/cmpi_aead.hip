@@ -268,6 +268,13 @@ void wipe_chw(std::map<std::pair<uint32_t, uint32_t>, void*>& chw) {
   chw.clear();
 }
 
+// host-side key-derived values (the combine's powers of H) zeroed before their map entries are released
+template <class M>
+void wipe_map(M& m) {
+  for (auto& kv : m) memset(&kv.second, 0, sizeof kv.second);
+  m.clear();
+}
+
 int ensure_buf(void** p, size_t* cap, size_t need) {
   if (need <= *cap) return CMPI_OK;
   if (*p) (void)hipFree(*p);
@@ -535,7 +542,12 @@ int launch_gcm_combine(const cmpi_ctx* c, cmpi::dev::GcmCombineArgs& ca, uint32_
 std::atomic<int> g_lane_pair{2};
 template <int L, bool DEC>
 int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size_t lds, hipStream_t st) {
-  const int pr = L == 4 ? g_lane_pair.load() : 0;  // the line-aligned store forms exist for L = 4
+  // the line-aligned store forms exist for L = 4 and pay off on batches that stream HBM; a small
+  // batch's single round of waves ran ~1 us longer with them (16 x 100 B: 9.9 -> 11.1 us)
+  // (hook values 3 / 4: the select / branch form on every batch, for the parity tests)
+  const bool big = (uint64_t)a.ngroups * (uint64_t)L >= (uint64_t)grid * kGcmThreads;
+  const int h = g_lane_pair.load();
+  const int pr = L != 4 ? 0 : h >= 3 ? (h == 3 ? 2 : 1) : big ? h : 0;
   auto fn = pr == 2   ? cmpi::dev::gcm_lane_kernel<L, DEC, (L == 4 ? 2 : 0)>
             : pr == 1 ? cmpi::dev::gcm_lane_kernel<L, DEC, (L == 4 ? 1 : 0)>
                       : cmpi::dev::gcm_lane_kernel<L, DEC, 0>;
@@ -1348,6 +1360,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   wipe_dev(c->stage, c->stage_cap);
   wipe_dev(c->dt, sizeof(DevTables));  // round keys, H, GHASH tables
   wipe_chw(c->chw);                     // (waits for the memsets above too)
+  wipe_map(c->mj);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
@@ -1402,7 +1415,7 @@ void cmpi_debug_set_stream_mode(int mode) { g_stream_mode.store(mode >= 0 && mod
 void cmpi_debug_set_host_spin(int mode) { g_host_spin.store(mode >= 0 && mode <= 3 ? mode : 0); }
 
 void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }
-void cmpi_debug_set_lane_pair(int on) { g_lane_pair.store(on == 1 || on == 2 ? on : 0); }
+void cmpi_debug_set_lane_pair(int on) { g_lane_pair.store(on >= 1 && on <= 4 ? on : 0); }
 void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 || threads == 1024 ? threads : 0); }
 
 // Timing events without the system-scope release fence (hipEventDisableSystemFence): a default
@@ -1641,7 +1654,7 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
   {
     std::lock_guard<std::mutex> lk(dst->mu);
     wipe_chw(dst->chw);
-    dst->mj.clear();
+    wipe_map(dst->mj);
     dst->dev_keys = true;
     memset(dst->key, 0, 16);
     memset(&dst->rk, 0, sizeof dst->rk);
@@ -1692,7 +1705,7 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
   }
   std::lock_guard<std::mutex> lk(c->mu);
   wipe_chw(c->chw);
-  c->mj.clear();
+  wipe_map(c->mj);
   memcpy(c->key, key, 16);
   cmpi::aes128_expand_words(key, c->rk.w);
   cmpi::aes128_dec_words(c->rk.w, c->drk.w);

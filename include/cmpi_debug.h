@@ -38,8 +38,9 @@ void cmpi_debug_event_free(void* ev);
  * CU, else 1024), 512 or 1024 forced (the chunk plan then assumes that many waves per CU). */
 void cmpi_debug_set_flow_threads(int threads);
 /* gcm_lane_kernel (L = 4) record stores grouped by 128-byte output line (each line stored whole in
- * the step that completes it): 2 = predicated selects (default), 1 = branches, 0 = a store per
- * step. */
+ * the step that completes it), on batches of at least one group per thread of the grid: 2 =
+ * predicated selects (default), 1 = branches, 0 = a store per step; 3 / 4 = the select / branch
+ * form on every batch (tests). */
 void cmpi_debug_set_lane_pair(int on);
 /* FLOW kernel: a batch whose chunks all fit one workgroup finishes its tags in-kernel (1, default)
  * or through the XOR-combine launch (0). */

@@ -79,12 +79,12 @@ def test_openssl_vectors(golden):
         assert st[0] == 1 and back[0].tobytes() == pt[0].tobytes()
 
 
-@pytest.mark.parametrize("pair", [0, 1, 2])
+@pytest.mark.parametrize("pair", [0, 3, 4])
 @pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 31, 48, 100, 1024, 1040, 4096, 4097, 65535])
 @pytest.mark.parametrize("plan", [(0, 0), (1, 1), (2, 1), (4, 1), (4, 3), (1, 2), (2, 7)])
 def test_batch_parity_plans(n, plan, pair):
-    """Every lane plan, with the lane kernel's main loop one slot or two slots per iteration
-    (cmpi_debug_set_lane_pair)."""
+    """Every lane plan, with the lane kernel's record stores one per step or grouped by output
+    line in both forms, forced on these small batches (cmpi_debug_set_lane_pair 3 / 4)."""
     aead.force_plan(*plan)
     aead.N.lib().cmpi_debug_set_lane_pair(pair)
     nrec = 24 if n <= 4096 else 4
