@@ -4,8 +4,9 @@ single 64 KiB messages, 3 x 100000 B, 1 x 8 MiB, 32 x 256 KiB) and two ragged on
 65536 x 1000 B on the lane kernel) and short records (1000 B, 100 B; few of them).
 
     [AB_SHAPES=65536x1024,65536x4096] python tools/flow_ab.py <libA.so> <libB.so> [rounds]
-    (a build may carry test hooks: path/libcmpi_aead.so@lane_aligned=0 calls
-     cmpi_debug_set_lane_aligned(0) in that build's processes)
+    (a build may carry test hooks: path/libcmpi_aead.so@lane_pair=0 calls
+     cmpi_debug_set_lane_pair(0) in that build's processes; force_wide=1:8 calls
+     cmpi_debug_force_wide(1, 8))
 
 Each (round, build) runs in its own process (`--child <lib>`): per shape, 0.3 s of warm-up, then
 seal and open kernel times from fence-free HIP events over 30 back-to-back calls; the parent prints
@@ -39,8 +40,9 @@ def child() -> None:
     from cryptmpi_2022_amd import _native as N
 
     for kv in filter(None, os.environ.get("AB_HOOKS", "").split(",")):
-        k, v = kv.split("=")
-        getattr(N.lib(), "cmpi_debug_set_" + k)(int(v))
+        k, v = kv.split("=")  # set_<k>(v), or force_<k>(a, b) for "force_wide=1:8"
+        args = [int(x) for x in v.split(":")]
+        getattr(N.lib(), "cmpi_debug_" + (k if k.startswith("force_") else "set_" + k))(*args)
 
     out = {}
     for name, (n, nrec) in shapes().items():
