@@ -1566,6 +1566,11 @@ int cmpi_ctr_xor_host(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t
   if (!c || !out || !in || !ctr_block) return fail(CMPI_EINVAL, "null argument");
   if (skip > 15) return fail(CMPI_EINVAL, "skip must be 0..15");
   if (n == 0) return CMPI_OK;
+  if (n + skip <= cmpi::dev::kSvcMaxStreamLen) {  // the context's message service, when started
+    DeviceGuard dg(c->device);
+    std::unique_lock<std::mutex> lk(c->hmu);
+    if (c->svc) return svc_ctr_host(c, *c->svc, out, in, n, ctr_block, skip);
+  }
   return host_stream_op(c, out, in, n, skip, [&](uint8_t* di, uint8_t* dout, size_t span, hipStream_t s) {
     return ctr_launch(c, dout, di, (size_t)skip + n, ctr_block, s);
   });

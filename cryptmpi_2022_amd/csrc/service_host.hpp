@@ -183,6 +183,22 @@ int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc]
   return CMPI_OK;
 }
 
+// The page-locked bounce buffer of pageable messages, at least `need` bytes.  hmu held.
+int svc_bounce(Svc& S, size_t need) {
+  if (S.bcap >= need) return CMPI_OK;
+  if (S.bounce) {
+    memset(S.bounce, 0, S.bcap);  // its last message
+    (void)hipHostFree(S.bounce);
+  }
+  S.bounce = nullptr;
+  S.bcap = 0;
+  const size_t cap = std::max<size_t>(need, (size_t)1 << 20);
+  if (hipHostMalloc((void**)&S.bounce, cap, hipHostMallocDefault) != hipSuccess)
+    return fail(CMPI_ENOMEM, "hipHostMalloc service bounce failed");
+  S.bcap = cap;
+  return CMPI_OK;
+}
+
 // One message through the service.  hmu held; pageable buffers go through the bounce.
 template <bool DEC>
 int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const uint8_t* nonce, size_t len,
@@ -192,15 +208,8 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
   void* dout = pinned_dev_ptr(out);
   uint8_t* hout = nullptr;
   const size_t bi = (in_rec + 255) & ~(size_t)255, need = bi + out_rec + 256;
-  if ((!din || !dout) && S.bcap < need) {
-    if (S.bounce) (void)hipHostFree(S.bounce);
-    S.bounce = nullptr;
-    S.bcap = 0;
-    const size_t cap = std::max<size_t>(need, (size_t)1 << 20);
-    if (hipHostMalloc((void**)&S.bounce, cap, hipHostMallocDefault) != hipSuccess)
-      return fail(CMPI_ENOMEM, "hipHostMalloc service bounce failed");
-    S.bcap = cap;
-  }
+  if (!din || !dout)
+    if (int rc = svc_bounce(S, need)) return rc;
   if (!din) {
     if (in_rec) memcpy(S.bounce, in, in_rec);
     din = pinned_dev_ptr(S.bounce);
@@ -233,9 +242,9 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
 // out = in ^ mask, kSvcCtr out = in ^ E_K(ctr + j) (in null: the keystream); device (or page-locked)
 // buffers, len <= kSvcMaxStreamLen.  Synchronous: the bytes are in `out` when it returns.  hmu held.
 int svc_stream(const cmpi_ctx* c, Svc& S, uint32_t op, uint8_t* out, const uint8_t* in, const uint8_t* mask,
-               const uint8_t ctr[16], size_t len) {
+               const uint8_t ctr[16], size_t len, unsigned skip = 0) {
   if (len == 0) return CMPI_OK;
-  if (len > cmpi::dev::kSvcMaxStreamLen) return fail(CMPI_EINVAL, "served counter-mode op over 64 KiB");
+  if (len + skip > cmpi::dev::kSvcMaxStreamLen) return fail(CMPI_EINVAL, "served counter-mode op over 64 KiB");
   const uint64_t pi = (uint64_t)(uintptr_t)in, po = (uint64_t)(uintptr_t)out;
   uint32_t d[cmpi::dev::kSvcDesc] = {op, (uint32_t)len, (uint32_t)pi, (uint32_t)(pi >> 32), (uint32_t)po,
                                      (uint32_t)(po >> 32)};
@@ -245,6 +254,7 @@ int svc_stream(const cmpi_ctx* c, Svc& S, uint32_t op, uint8_t* out, const uint8
     d[7] = (uint32_t)(pm >> 32);
   } else {
     const uint64_t h = cmpi::be64(ctr), l = cmpi::be64(ctr + 8);
+    d[6] = skip;  // keystream bytes skipped before the message's first byte (0..15)
     d[8] = (uint32_t)h;
     d[9] = (uint32_t)(h >> 32);
     d[10] = (uint32_t)l;
@@ -252,6 +262,31 @@ int svc_stream(const cmpi_ctx* c, Svc& S, uint32_t op, uint8_t* out, const uint8
   }
   uint32_t w[5];
   return svc_exec(c, S, d, w);
+}
+
+// cmpi_ctr_xor_host through a CTR context's service: page-locked buffers in place, pageable ones
+// through the service's bounce buffer.  hmu held.
+int svc_ctr_host(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, size_t n, const uint8_t cb[16],
+                 unsigned skip) {
+  void* din = pinned_dev_ptr(in);
+  void* dout = pinned_dev_ptr(out);
+  uint8_t* hout = nullptr;
+  const size_t bi = (n + 255) & ~(size_t)255;
+  if (!din || !dout)
+    if (int rc = svc_bounce(S, bi + n + 256)) return rc;
+  if (!din) {
+    memcpy(S.bounce, in, n);
+    din = pinned_dev_ptr(S.bounce);
+  }
+  if (!dout) {
+    hout = S.bounce + bi;
+    dout = pinned_dev_ptr(hout);
+  }
+  if (!din || !dout) return fail(CMPI_EHIP, "service buffers have no device address");
+  const int rc = svc_stream(c, S, cmpi::dev::kSvcCtr, static_cast<uint8_t*>(dout), static_cast<const uint8_t*>(din),
+                            nullptr, cb, n, skip);
+  if (!rc && hout) memcpy(out, hout, n);
+  return rc;
 }
 
 }  // namespace

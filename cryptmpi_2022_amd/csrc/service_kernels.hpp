@@ -217,7 +217,23 @@ __device__ __forceinline__ void svc_stream_op(const SvcArgs& s, const RowLanes& 
   uint8_t* outp = reinterpret_cast<uint8_t*>(lds_ptr64(kSvcX + 24u));
   const uint8_t* mask = reinterpret_cast<const uint8_t*>(lds_ptr64(kSvcX + 32u));
   const uint64_t chi = lds_ptr64(kSvcX + 40u), clo = lds_ptr64(kSvcX + 48u);
-  const uint32_t nblk = (len + 15u) >> 4;
+  // kSvcCtr: word 6 = keystream bytes skipped before the message (cmpi_ctr_xor_host's `skip`)
+  const uint32_t skip = op == kSvcCtr ? __builtin_amdgcn_readfirstlane(lds32(kSvcX + 32u)) : 0u;
+  if (skip) {  // byte-granular: keystream block j covers message bytes [16j - skip, 16j + 16 - skip)
+    for (uint32_t j = threadIdx.x; j < (skip + len + 15u) >> 4; j += kSvcThreads) {
+      uint32_t w0, w1, w2, w3;
+      ctr_words(chi, clo, j, w0, w1, w2, w3);
+      aes128_enc(s.rk, rl, w0, w1, w2, w3);
+      const uint32_t ks[4] = {w0, w1, w2, w3};
+#pragma unroll
+      for (uint32_t b = 0; b < 16u; ++b) {
+        const int32_t i = (int32_t)(16u * j + b) - (int32_t)skip;
+        if (i >= 0 && i < (int32_t)len)
+          outp[i] = (uint8_t)((inp ? inp[i] : 0u) ^ (uint8_t)(ks[b >> 2] >> (8u * (b & 3u))));
+      }
+    }
+  }
+  const uint32_t nblk = skip ? 0u : (len + 15u) >> 4;
   for (uint32_t j = threadIdx.x; j < nblk; j += kSvcThreads) {
     const uint32_t off = 16u * j, rem = len - off < 16u ? len - off : 16u;
     u32x4 ks;

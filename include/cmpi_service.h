@@ -23,7 +23,8 @@
  * exit: call cmpi_service_stop first, or keep idle_us short.
  * On an AES-128-CTR context the service serves CryptMPI's counter-mode small messages instead
  * (cmpi_ctrmode.h, cmpi_ring.h: the 702 ring XOR, send.c:1273-1465; the receiver's premask and
- * mask XOR, recv.c:954-1023, :1107-1220; the 700 / 702 direct CTR of messages up to 64 KiB):
+ * mask XOR, recv.c:954-1023, :1107-1220; the 700 / 702 direct CTR of messages up to 64 KiB;
+ * cmpi_ctr_xor_host, the EVP shim's EVP_EncryptUpdate, on host buffers):
  * each such op of at most 64 KiB is posted to the kernel instead of launched, and is complete
  * when the call returns.  It runs outside stream order, so the call first waits for the work
  * already queued on its `stream` (and for the ring's last fill); bytes, headers and ring state

@@ -9,6 +9,8 @@ Every test runs twice: with a launch per op, and with the context's message serv
 ring_host.hpp Served)."""
 import random
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -190,3 +192,29 @@ def test_served_ops_follow_the_stream(ctx):
     ctrmode.recv702(ctx, IV32, hdr, out, ct2)
     assert host(out).tobytes() == pt.tobytes()
     s.close()
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 1000, 4096, 65536 - 15])
+@pytest.mark.parametrize("skip", [0, 1, 9, 15])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_ctr_xor_host_skip(ctx, n, skip, pinned):
+    """cmpi_ctr_xor_host (the EVP shim's EVP_EncryptUpdate on a CTR context): the message starts
+    `skip` bytes into the counter block's keystream; host buffers pageable or page-locked — served
+    by the resident kernel when the context runs one (byte-granular form for skip > 0)."""
+    import ctypes
+
+    from cryptmpi_2022_amd import _native as N
+
+    cb = bytes(range(200, 216))
+    pt = splitmix64_bytes(n * 31 + skip, n)
+    if pinned:
+        src_t = torch.from_numpy(pt.copy()).pin_memory()
+        dst_t = torch.full((n,), 0xEE, dtype=torch.uint8).pin_memory()
+        src, dst = src_t.numpy(), dst_t.numpy()
+    else:
+        src, dst = pt.copy(), np.full(n, 0xEE, np.uint8)
+    cbb = (ctypes.c_uint8 * 16).from_buffer_copy(cb)
+    N.check(N.lib().cmpi_ctr_xor_host(ctx.handle, ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(src.ctypes.data),
+                                      n, cbb, skip))
+    ks = oracle.ctr_xor(KEY, cb, bytes(skip + n))[skip:]
+    assert dst.tobytes() == bytes(a ^ b for a, b in zip(pt.tobytes(), ks))

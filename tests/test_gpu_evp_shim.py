@@ -17,8 +17,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHIM = os.path.join(ROOT, "cryptmpi_2022_amd", "libcmpi_evp.so")
 
 
+@pytest.mark.parametrize("service", [False, True])
 @pytest.mark.parametrize("p,n", [(8, 4096), (3, 1001), (2, 0)])
-def test_c_client_naive_alltoall(tmp_path, p, n):
+def test_c_client_naive_alltoall(tmp_path, p, n, service):
+    """The C client of CryptMPI's call sites; with CMPI_EVP_SERVICE_US the AEAD seals and the CTR
+    EncryptUpdates (the second one starting mid-block) are served by the contexts' resident kernels."""
     exe = tmp_path / "evp_client"
     subprocess.check_call(["gcc", "-O1", "-o", str(exe), os.path.join(ROOT, "tests", "evp_client.c"),
                            f"-L{os.path.dirname(SHIM)}", "-lcmpi_evp", f"-Wl,-rpath,{os.path.dirname(SHIM)}"])
@@ -28,7 +31,11 @@ def test_c_client_naive_alltoall(tmp_path, p, n):
     inp = tmp_path / "in.bin"
     inp.write_bytes(key + nonces.tobytes() + send.tobytes())
     outp = tmp_path / "out.bin"
-    r = subprocess.run([str(exe), str(p), str(n), str(inp), str(outp)], capture_output=True, text=True)
+    env = dict(os.environ)
+    if service:
+        env["CMPI_EVP_SERVICE_US"] = "2000"
+    r = subprocess.run([str(exe), str(p), str(n), str(inp), str(outp)], capture_output=True, text=True, env=env,
+                       timeout=120)
     assert r.returncode == 0, (r.returncode, r.stderr)
     out = outp.read_bytes()
     wire_len = (n + 28) * p

@@ -470,6 +470,30 @@ int main(int argc, char** argv) {
       CK(hipFree(dbk));
       CK(hipFree(dmask));
     }
+    {  // EVP_EncryptUpdate on a CTR context through the shim = cmpi_ctr_xor_host on the MPI user
+       // buffer: 4 KiB page-locked, a launch per call vs the context's resident service
+      uint8_t *hin, *hout;
+      CK(hipHostMalloc((void**)&hin, 4096, hipHostMallocDefault));
+      CK(hipHostMalloc((void**)&hout, 4096, hipHostMallocDefault));
+      memset(hin, 0x3c, 4096);
+      uint8_t cb[16];
+      for (int i = 0; i < 16; ++i) cb[i] = (uint8_t)(i * 5);
+      put("ctr_host_4k_launch_us", median_us(iters, [&] { CM(cmpi_ctr_xor_host(cc, hout, hin, 4096, cb, 0)); }));
+      CM(cmpi_service_start(cc, 20000));
+      put("ctr_host_4k_served_us", median_us(iters, [&] { CM(cmpi_ctr_xor_host(cc, hout, hin, 4096, cb, 0)); }));
+      std::vector<uint8_t> pg_in(4096, 0x3c), pg_out(4096);
+      put("ctr_pageable_4k_served_us",
+          median_us(iters, [&] { CM(cmpi_ctr_xor_host(cc, pg_out.data(), pg_in.data(), 4096, cb, 0)); }));
+      CM(cmpi_service_stop(cc));
+      put("ctr_pageable_4k_launch_us",
+          median_us(iters, [&] { CM(cmpi_ctr_xor_host(cc, pg_out.data(), pg_in.data(), 4096, cb, 0)); }));
+      if (memcmp(pg_out.data(), hout, 4096)) {
+        fprintf(stderr, "ctr host served / launched outputs differ\n");
+        return 1;
+      }
+      CK(hipHostFree(hin));
+      CK(hipHostFree(hout));
+    }
     cmpi_702_sender_free(snd);
     cmpi_ctx_free(cc);
   }
