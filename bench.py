@@ -1134,7 +1134,8 @@ def c_timed_latency(iters: int = 300) -> dict:
             "c702_4k_send_call_cpu_us", "c702_4k_recv_direct_call_cpu_us", "c702_4k_served_send_only_us",
             "c702_4k_served_recv_mask_us", "c702_4k_served_send_recv_nomask_us",
             "c702_4k_served_send_premask_recv_us", "ctr_host_4k_launch_us", "ctr_host_4k_served_us",
-            "ctr_pageable_4k_launch_us", "ctr_pageable_4k_served_us", "svc_pinned_seal_1k_us",
+            "ctr_pageable_4k_launch_us", "ctr_pageable_4k_served_us", "ecb_16b_launch_us", "ecb_16b_served_us",
+            "svc_pinned_seal_1k_us",
             "svc_pinned_open_1k_us", "svc_pinned_seal_64k_us", "svc_pinned_open_64k_us", "c602_8m_seal_per_outer_us",
             "c602_8m_seal_whole_us", "c602_8m_open_per_outer_us")
     out = {k: d[k] for k in keep if k in d}

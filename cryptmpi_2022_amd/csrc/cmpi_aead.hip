@@ -1579,6 +1579,11 @@ int cmpi_ctr_xor_host(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t
 int cmpi_ecb_encrypt_host(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t nblocks) {
   if (!c || !out || !in) return fail(CMPI_EINVAL, "null argument");
   if (nblocks == 0) return CMPI_OK;
+  if (nblocks * 16 <= cmpi::dev::kSvcMaxStreamLen && c->alg == CMPI_AES_128_ECB) {  // served, when started
+    DeviceGuard dg(c->device);
+    std::unique_lock<std::mutex> lk(c->hmu);
+    if (c->svc) return svc_ctr_host(c, *c->svc, out, in, nblocks * 16, nullptr, 0, cmpi::dev::kSvcEcb);
+  }
   return host_stream_op(c, out, in, nblocks * 16, 0, [&](uint8_t* di, uint8_t* dout, size_t span, hipStream_t s) {
     return cmpi_ecb_encrypt(c, dout, di, nblocks, s);
   });

@@ -83,8 +83,9 @@ const size_t kIdleCap = env_size("CMPI_EVP_CTX_CACHE", 16);
 const long kWindowUs = (long)env_size("CMPI_EVP_COALESCE_US", 30);
 // CMPI_EVP_SERVICE_US = n > 0: every context serves its single messages from the resident message
 // service (include/cmpi_service.h), which returns its CUs after n us without messages — the AEAD
-// contexts' seal / open and the CTR cipher contexts' EVP_EncryptUpdate of up to 64 KiB (the 700 /
-// 702 per-message calls).  0 (default): one kernel launch per EVP call.
+// contexts' seal / open and the CTR / ECB cipher contexts' EVP_EncryptUpdate of up to 64 KiB (the
+// 700 / 702 per-message calls, the 602 sub-key derivation).  0 (default): one kernel launch per
+// EVP call.
 const size_t kServiceUs = env_size("CMPI_EVP_SERVICE_US", 0);
 // idle limit of the drop-in's services: a resident kernel delays device-wide synchronisation
 // (hipDeviceSynchronize) of the whole process until it idles out (cmpi_service.h)
@@ -415,7 +416,7 @@ int cipher_init(EVP_CIPHER_CTX* ctx, const EVP_CIPHER* cipher, ENGINE* engine, c
       if (cmpi_ctx_rekey(ctx->c, key, 16, nullptr) != CMPI_OK) return 0;
     } else if (!(ctx->c = cmpi_ctx_new(ctx->alg, key, 16, 0, pick_device()))) {
       return 0;
-    } else if (kServiceUs && ctx->alg == CMPI_AES_128_CTR &&
+    } else if (kServiceUs && (ctx->alg == CMPI_AES_128_CTR || ctx->alg == CMPI_AES_128_ECB) &&
                cmpi_service_start(ctx->c, (uint32_t)std::min<size_t>(kServiceUs, kServiceCapUs)) != CMPI_OK) {
       cmpi_ctx_free(ctx->c);
       ctx->c = nullptr;

@@ -252,7 +252,7 @@ int svc_stream(const cmpi_ctx* c, Svc& S, uint32_t op, uint8_t* out, const uint8
     const uint64_t pm = (uint64_t)(uintptr_t)mask;
     d[6] = (uint32_t)pm;
     d[7] = (uint32_t)(pm >> 32);
-  } else {
+  } else if (op == cmpi::dev::kSvcCtr) {
     const uint64_t h = cmpi::be64(ctr), l = cmpi::be64(ctr + 8);
     d[6] = skip;  // keystream bytes skipped before the message's first byte (0..15)
     d[8] = (uint32_t)h;
@@ -264,10 +264,11 @@ int svc_stream(const cmpi_ctx* c, Svc& S, uint32_t op, uint8_t* out, const uint8
   return svc_exec(c, S, d, w);
 }
 
-// cmpi_ctr_xor_host through a CTR context's service: page-locked buffers in place, pageable ones
-// through the service's bounce buffer.  hmu held.
+// cmpi_ctr_xor_host (op kSvcCtr) / cmpi_ecb_encrypt_host (kSvcEcb, cb unused) through the context's
+// service: page-locked buffers in place, pageable ones through the service's bounce buffer.  hmu
+// held.
 int svc_ctr_host(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, size_t n, const uint8_t cb[16],
-                 unsigned skip) {
+                 unsigned skip, uint32_t op = cmpi::dev::kSvcCtr) {
   void* din = pinned_dev_ptr(in);
   void* dout = pinned_dev_ptr(out);
   uint8_t* hout = nullptr;
@@ -283,8 +284,8 @@ int svc_ctr_host(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, siz
     dout = pinned_dev_ptr(hout);
   }
   if (!din || !dout) return fail(CMPI_EHIP, "service buffers have no device address");
-  const int rc = svc_stream(c, S, cmpi::dev::kSvcCtr, static_cast<uint8_t*>(dout), static_cast<const uint8_t*>(din),
-                            nullptr, cb, n, skip);
+  const int rc = svc_stream(c, S, op, static_cast<uint8_t*>(dout), static_cast<const uint8_t*>(din), nullptr, cb, n,
+                            skip);
   if (!rc && hout) memcpy(out, hout, n);
   return rc;
 }
@@ -295,8 +296,8 @@ extern "C" {
 
 int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
   if (!c) return fail(CMPI_EINVAL, "null ctx");
-  if (c->alg != CMPI_AES_128_GCM && c->alg != CMPI_AES_128_CTR)
-    return fail(CMPI_EINVAL, "the message service serves AES-128-GCM and AES-128-CTR contexts");
+  if (c->alg != CMPI_AES_128_GCM && c->alg != CMPI_AES_128_CTR && c->alg != CMPI_AES_128_ECB)
+    return fail(CMPI_EINVAL, "the message service serves AES-128-GCM, -CTR and -ECB contexts");
   if (c->dev_keys) return fail(CMPI_EINVAL, "the message service needs a host-keyed context");
   DeviceGuard dg(c->device);
   std::lock_guard<std::mutex> lk(c->hmu);

@@ -34,7 +34,8 @@
 //           and the host takes a pair only with the new seq in it, so a pair cannot tear; the host
 //           writes a seal's tag into out + len itself.
 //   counter-mode ops (CTR contexts: the 702 / 700 small-message XORs, send.c:1273-1465,
-//           recv.c:954-1023, :1187-1220): kSvcXor out = in ^ mask, kSvcCtr out = in ^ E_K(ctr + j)
+//           recv.c:954-1023, :1187-1220): kSvcXor out = in ^ mask, kSvcCtr out = in ^ E_K(ctr + j),
+//           kSvcEcb out = E_K(in) per 16-byte block (the 602 sub-key K' = AES_K(V), send.c:583)
 //           (in null: the keystream), at most kSvcMaxStreamLen bytes, served by the leader's
 //           workgroup alone and completed like a seal (status 1, no tag).
 // Every wave's wait loop is bounded by the wall clock: the grid drains even if the host vanishes.
@@ -48,7 +49,7 @@ namespace dev {
 constexpr uint32_t kSvcThreads = 512u;
 constexpr uint32_t kSvcGroups = 8u;      // workgroups (one per XCD when the chip is free)
 constexpr uint32_t kSvcMaxChunks = 64u;  // kSvcGroups x 8 waves
-constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u, kSvcXor = 3u, kSvcCtr = 4u;
+constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u, kSvcXor = 3u, kSvcCtr = 4u, kSvcEcb = 5u;
 // descriptor words: op, len, in lo/hi, out lo/hi, then the op's own: GCM nonce[3] at 6..8, XOR
 // mask lo/hi at 6..7, CTR counter block as big-endian halves hi lo/hi, lo lo/hi at 8..11
 constexpr uint32_t kSvcDesc = 12u;
@@ -237,6 +238,13 @@ __device__ __forceinline__ void svc_stream_op(const SvcArgs& s, const RowLanes& 
   for (uint32_t j = threadIdx.x; j < nblk; j += kSvcThreads) {
     const uint32_t off = 16u * j, rem = len - off < 16u ? len - off : 16u;
     u32x4 ks;
+    if (op == kSvcEcb) {  // whole blocks (the host sends multiples of 16)
+      const u32x4 b = ld_blk(inp + off);
+      uint32_t w0 = b[0], w1 = b[1], w2 = b[2], w3 = b[3];
+      aes128_enc(s.rk, rl, w0, w1, w2, w3);
+      st_blk(outp + off, u32x4{w0, w1, w2, w3});
+      continue;
+    }
     if (op == kSvcXor) {
       ks = rem == 16u ? ld_blk(mask + off) : load_partial(mask + off, rem);
     } else {

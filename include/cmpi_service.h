@@ -29,7 +29,9 @@
  * when the call returns.  It runs outside stream order, so the call first waits for the work
  * already queued on its `stream` (and for the ring's last fill); bytes, headers and ring state
  * are those of the launched form.
- * Host-keyed AES-128-GCM and AES-128-CTR contexts only (CMPI_EINVAL otherwise).  cmpi_ctx_rekey and
+ * On an AES-128-ECB context it serves cmpi_ecb_encrypt_host of up to 64 KiB (the 602 sub-key
+ * derivation, send.c:583).
+ * Host-keyed AES-128-GCM, -CTR and -ECB contexts only (CMPI_EINVAL otherwise).  cmpi_ctx_rekey and
  * cmpi_ctx_rekey_subkey stop a running service (the next message restarts it with the new key;
  * a device-keyed context ends the service).  cmpi_ctx_free stops it.
  */

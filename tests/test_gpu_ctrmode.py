@@ -218,3 +218,24 @@ def test_ctr_xor_host_skip(ctx, n, skip, pinned):
                                       n, cbb, skip))
     ks = oracle.ctr_xor(KEY, cb, bytes(skip + n))[skip:]
     assert dst.tobytes() == bytes(a ^ b for a, b in zip(pt.tobytes(), ks))
+
+
+@pytest.mark.parametrize("served", [False, True])
+@pytest.mark.parametrize("nblocks", [1, 7, 4096])
+def test_ecb_host_served(served, nblocks):
+    """cmpi_ecb_encrypt_host (the shim's EVP_EncryptUpdate on an ECB context: the 602 sub-key
+    K' = AES_K(V), send.c:583) launched and served by the ECB context's resident kernel."""
+    import ctypes
+
+    from cryptmpi_2022_amd import _native as N
+
+    c = aead.CipherCtx(KEY, "aes-128-ecb")
+    if served:
+        c.service_start()
+    pt = splitmix64_bytes(0xEC + nblocks, 16 * nblocks)
+    out = np.zeros(16 * nblocks, np.uint8)
+    N.check(N.lib().cmpi_ecb_encrypt_host(c.handle, ctypes.c_void_p(out.ctypes.data),
+                                          ctypes.c_void_p(pt.ctypes.data), nblocks))
+    assert out.tobytes() == oracle.ecb_encrypt(KEY, pt.tobytes())
+    if served:
+        c.service_stop()

@@ -493,6 +493,19 @@ int main(int argc, char** argv) {
       }
       CK(hipHostFree(hin));
       CK(hipHostFree(hout));
+      // the 602 sub-key derivation, EVP_EncryptUpdate(ctx_enc, K', V, 16) on an ECB context
+      // (send.c:583), pageable 16 bytes: a launch per call vs the ECB context's service
+      cmpi_ctx* ce = cmpi_ctx_new(CMPI_AES_128_ECB, key2, 16, 0, 0);
+      uint8_t v16[16] = {1, 2, 3}, k16[16], k16b[16];
+      put("ecb_16b_launch_us", median_us(iters, [&] { CM(cmpi_ecb_encrypt_host(ce, k16, v16, 1)); }));
+      CM(cmpi_service_start(ce, 20000));
+      put("ecb_16b_served_us", median_us(iters, [&] { CM(cmpi_ecb_encrypt_host(ce, k16b, v16, 1)); }));
+      CM(cmpi_service_stop(ce));
+      cmpi_ctx_free(ce);
+      if (memcmp(k16, k16b, 16)) {
+        fprintf(stderr, "ecb served / launched outputs differ\n");
+        return 1;
+      }
     }
     cmpi_702_sender_free(snd);
     cmpi_ctx_free(cc);
