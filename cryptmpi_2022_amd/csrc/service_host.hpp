@@ -15,9 +15,33 @@ namespace {
 constexpr size_t kSvcMaxLen = (size_t)512 << 10;  // 64 chunks of 8 steps
 constexpr uint64_t kSvcLifeUs = 100000;           // relaunched at least every 100 ms
 
-struct Svc {
+// Stream slots of a device's services.  HIP maps the streams of one priority onto at most
+// GPU_MAX_HW_QUEUES (4) hardware queues, and a resident kernel holds its queue: with a stream per
+// service, the fifth context's service shared a queue with another's resident kernel and waited
+// for it to idle out (20 ms at the EVP shim's cap, tools/svc_many_probe.py).  So the services of
+// a device share kSvcSlots greatest-priority streams, one resident generation per slot: a
+// context whose service launches on a slot held by another's kicks that generation (the kick
+// word its leader polls; a posted message is always served first) and queues behind it.
+constexpr int kSvcSlots = 4;
+constexpr int kSvcMaxDevices = 16;
+struct Svc;
+struct SvcSlot {
+  std::mutex m;
   hipStream_t st = nullptr;
-  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..15] (four 16-B chunks), done [32..44]
+  Svc* owner = nullptr;  // the service whose generation was launched last on this slot
+};
+SvcSlot& svc_slot(int dev, int i) {
+  static SvcSlot slots[kSvcMaxDevices][kSvcSlots];
+  return slots[dev][i];
+}
+std::atomic<uint32_t> g_svc_next_slot[kSvcMaxDevices];
+
+struct Svc {
+  hipStream_t st = nullptr;    // the slot's stream (shared; not owned)
+  int dev = 0, slot = 0;
+  hipEvent_t ev = nullptr;     // recorded after this service's last launch
+  bool launched = false;
+  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..15] (four 16-B chunks), kick [16], done [32..44]
   uint32_t* dw = nullptr;      // its device address
   uint32_t* go = nullptr;      // device control words (64 B), counter (at +64), partials (at +128)
   cmpi::dev::u32x4* wts = nullptr;  // device chunk weights (4 x 64 x 4 blocks)
@@ -29,8 +53,16 @@ struct Svc {
   bool running = false;
   uint32_t idle_us = 2000;
   uint32_t* ring() { return hw; }
+  uint32_t* kick() { return hw + 16; }
   uint32_t* done() { return hw + 32; }
 };
+
+// This service's last generation has left the device (its stream slot may already run another
+// context's generation behind it).
+int svc_drain(Svc& S) {
+  if (S.launched) HIP_TRY(hipEventSynchronize(S.ev));
+  return CMPI_OK;
+}
 
 // Post descriptor d[0..11] under `seq`: chunk c = {seq, d[3c..3c+2]} at ring[4c]; the words first,
 // then seq into every chunk (the kernel takes a chunk's words only with the new seq in all four).
@@ -56,7 +88,12 @@ void svc_wipe(Svc& S) {
 void svc_release(Svc& S) {
   svc_wipe(S);
   wipe_sync();  // the memsets before the frees
-  if (S.st) (void)hipStreamDestroy(S.st);
+  {
+    SvcSlot& sl = svc_slot(S.dev, S.slot);
+    std::lock_guard<std::mutex> g(sl.m);
+    if (sl.owner == &S) sl.owner = nullptr;
+  }
+  if (S.ev) (void)hipEventDestroy(S.ev);
   if (S.hw) (void)hipHostFree(S.hw);
   if (S.go) (void)hipFree(S.go);
   if (S.wts) (void)hipFree(S.wts);
@@ -89,9 +126,17 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
     if (int rc = svc_weights(c, S)) return rc;
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_service_kernel), c->device, cmpi::dev::kFlowLds);
   if (rc) return rc;
+  SvcSlot& sl = svc_slot(S.dev, S.slot);
+  std::lock_guard<std::mutex> g(sl.m);
+  DeviceGuard dg(S.dev);
+  if (!sl.st && lib_stream(&sl.st, true) != hipSuccess) return fail(CMPI_EHIP, "service stream creation failed");
+  S.st = sl.st;
+  if (sl.owner && sl.owner != &S)  // its generation (if still resident) leaves at its next poll
+    __atomic_store_n(sl.owner->kick(), sl.owner->gen, __ATOMIC_RELEASE);
   if ((rc = wait_keys(c, S.st))) return rc;  // tables of a re-key still in flight on the caller's stream
   cmpi::dev::SvcArgs a{};
   a.ring = S.dw;
+  a.kick = S.dw + 16;
   a.done = S.dw + 32;
   a.go = S.go;
   a.cnt = S.go + 16;
@@ -109,6 +154,9 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
   void* kargs[] = {&a};
   HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(cmpi::dev::gcm_service_kernel), dim3(cmpi::dev::kSvcGroups),
                           dim3(cmpi::dev::kSvcThreads), kargs, cmpi::dev::kFlowLds, S.st));
+  HIP_TRY(hipEventRecord(S.ev, S.st));
+  sl.owner = &S;
+  S.launched = true;
   S.running = true;
   return CMPI_OK;
 }
@@ -128,14 +176,15 @@ bool svc_done(Svc& S, uint32_t seq, uint32_t (&w)[5]) {
   return true;
 }
 
-// Stop a running service and drain its stream (ctx free, re-key, cmpi_service_stop).  hmu held.
+// Stop a running service and wait until its generation has left (ctx free, re-key,
+// cmpi_service_stop).  hmu held.
 int svc_stop_locked(Svc& S) {
-  if (!S.st) return CMPI_OK;
+  if (!S.launched) return CMPI_OK;
   if (S.running && !svc_exited(S)) {
     const uint32_t d[cmpi::dev::kSvcDesc] = {cmpi::dev::kSvcStop};
     svc_post(S, d, ++S.seq);
   }
-  HIP_TRY(hipStreamSynchronize(S.st));  // the kernel exits at its next poll
+  if (int rc = svc_drain(S)) return rc;  // the kernel exits at its next poll
   S.running = false;
   return CMPI_OK;
 }
@@ -153,8 +202,8 @@ int svc_shutdown_locked(cmpi_ctx* c) {
 // Post descriptor d as the next message (the service launched first if it is not running) and
 // wait for its completion words w (status, tag 0-3).  hmu held.
 int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc], uint32_t (&w)[5]) {
-  if (S.running && svc_exited(S)) {  // idled out since the last message
-    HIP_TRY(hipStreamSynchronize(S.st));
+  if (S.running && svc_exited(S)) {  // idled out (or kicked) since the last message
+    if (int rc = svc_drain(S)) return rc;
     S.running = false;
   }
   if (!S.running)
@@ -165,8 +214,8 @@ int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc]
   int relaunches = 0;
   for (uint32_t i = 1;; ++i) {
     if (svc_done(S, seq, w)) break;
-    if (svc_exited(S)) {  // the generation ended (lifetime): let every workgroup finish first
-      HIP_TRY(hipStreamSynchronize(S.st));
+    if (svc_exited(S)) {  // the generation ended (lifetime, kick): let every workgroup finish first
+      if (int rc = svc_drain(S)) return rc;
       S.running = false;
       if (svc_done(S, seq, w)) break;
       if (++relaunches > 2) return fail(CMPI_EHIP, "message service did not complete message %u", seq);
@@ -174,7 +223,7 @@ int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc]
       continue;
     }
     if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
-      const hipError_t e = hipStreamQuery(S.st);
+      const hipError_t e = hipEventQuery(S.ev);  // this generation (the slot's stream may hold others)
       if (e != hipSuccess && e != hipErrorNotReady) return fail(CMPI_EHIP, "service kernel: %s", hipGetErrorString(e));
       if (e == hipSuccess && !svc_done(S, seq, w) && !svc_exited(S))
         return fail(CMPI_EHIP, "service kernel ended without completing message %u", seq);
@@ -301,11 +350,14 @@ int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
   if (c->dev_keys) return fail(CMPI_EINVAL, "the message service needs a host-keyed context");
   DeviceGuard dg(c->device);
   std::lock_guard<std::mutex> lk(c->hmu);
+  if (c->device < 0 || c->device >= kSvcMaxDevices) return fail(CMPI_EINVAL, "device index beyond the service slots");
   if (!c->svc) c->svc = new Svc();
   Svc& S = *c->svc;
   S.idle_us = idle_us ? std::min<uint32_t>(idle_us, 1000000u) : 2000u;
-  if (S.st) return CMPI_OK;
-  if (lib_stream(&S.st, true) != hipSuccess ||
+  if (S.hw) return CMPI_OK;
+  S.dev = c->device;
+  S.slot = (int)(g_svc_next_slot[c->device].fetch_add(1) % kSvcSlots);
+  if (hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&S.hw, 256, hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&S.dw, S.hw, 0) != hipSuccess || hipMalloc((void**)&S.go, 256) != hipSuccess ||
       hipMalloc((void**)&S.wts, kSvcWtsBytes) != hipSuccess || hipMemset(S.go, 0, 256) != hipSuccess) {

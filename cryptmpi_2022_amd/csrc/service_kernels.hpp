@@ -15,7 +15,8 @@
 //           descriptor to device memory (go[4..12], write-through) and publishes go[1] = seq,
 //           both under a seqlock (go[3] odd while they change: a workgroup that sat out the last
 //           message may be reading them);
-//           on idle / lifetime / op STOP it publishes go[2] = 1, writes done[2] = gen and exits.
+//           on idle / lifetime / op STOP / a kick (the host word kick == gen: another context's
+//           service takes this stream slot) it publishes go[2] = 1, writes done[12] = gen and exits.
 //           A message whose chunks fit one workgroup is served by the leader's workgroup alone
 //           and not published (the others act only on a change of go[1]).
 //   others: poll go[] (write-through loads), run their share, exit on go[2].
@@ -58,6 +59,7 @@ constexpr uint32_t kSvcMaxStreamLen = 65536u;   // counter-mode ops: the 702 rin
 
 struct SvcArgs {
   const uint32_t* ring;  // page-locked host words (device address): chunks [4c] = seq, [4c+1..4c+3] = desc[3c..3c+2]
+  const uint32_t* kick;  // page-locked host word: == gen asks this generation to exit (its stream slot is wanted)
   uint32_t* done;        // page-locked host words: [0..9] five {seq, word} pairs (status, tag 0-3), [12] exited generation
   uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [3] seqlock version, [4..15] descriptor copy
   uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
@@ -296,8 +298,8 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
         for (;;) {
           asm volatile("" ::: "memory");  // a fresh read every pass
           u32x4 c0 = sys_load16(s.ring), c1 = sys_load16(s.ring + 4), c2 = sys_load16(s.ring + 8),
-                c3 = sys_load16(s.ring + 12);
-          asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));  // all four reads in flight together
+                c3 = sys_load16(s.ring + 12), ck = sys_load16(s.kick);
+          asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(ck));  // all five reads in flight together
           q = c0[0];
           if (q != cur) {
             if (c1[0] != q || c2[0] != q || c3[0] != q) continue;  // the host is between chunks: read again
@@ -309,7 +311,9 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
             break;
           }
           const uint64_t now = wall_clock64();
-          if (now - t_last > s.idle_ticks || now - t0 > s.life_ticks) {
+          // a posted message is always taken first (above); then a kick (another context's
+          // service wants this stream slot), idle or lifetime ends the generation
+          if (ck[0] == s.gen || now - t_last > s.idle_ticks || now - t0 > s.life_ticks) {
             ex = 1u;
             break;
           }

@@ -148,6 +148,31 @@ def test_service_two_contexts():
     b.close()
 
 
+def test_service_many_contexts_share_slots():
+    """More services than hardware queues (6 contexts, 4 stream slots): round-robin messages over
+    them are all bit-exact, and none waits for another context's resident kernel to idle out —
+    the slot's holder is kicked and the new generation queues behind it (was: ~20 ms per message
+    whose stream shared a queue with another resident kernel, tools/svc_many_probe.py)."""
+    keys = [bytes([k + 1] * 16) for k in range(6)]
+    ctxs = [aead.AeadCtx(k) for k in keys]
+    for c in ctxs:
+        c.service_start(500000)  # resident for the whole test unless kicked
+    lat = []
+    for i in range(36):
+        k = i % 6
+        pt = splitmix64_bytes(900 + i, 1000 + i).tobytes()
+        nonce = splitmix64_bytes(950 + i, 12).tobytes()
+        t0 = time.perf_counter()
+        got = ctxs[k].seal(nonce, pt)
+        lat.append(time.perf_counter() - t0)
+        assert got == oracle.gcm_seal(keys[k], nonce, pt), i
+        assert ctxs[k].open(nonce, got) == pt
+    for c in ctxs:
+        c.service_stop()
+        c.close()
+    assert max(lat[6:]) < 0.005, [round(v * 1e3, 2) for v in lat]
+
+
 def test_service_leaves_other_streams_free():
     """While the service kernel is resident, kernels on 8 other (normal-priority) streams and on the
     default stream complete without waiting for it: the service's stream sits in the greatest-
