@@ -88,8 +88,8 @@ void svc_wipe(Svc& S) {
 void svc_release(Svc& S) {
   svc_wipe(S);
   wipe_sync();  // the memsets before the frees
-  {
-    SvcSlot& sl = svc_slot(S.dev, S.slot);
+  for (int i = 0; i < kSvcSlots; ++i) {  // every slot that still names this service (it moves between slots)
+    SvcSlot& sl = svc_slot(S.dev, i);
     std::lock_guard<std::mutex> g(sl.m);
     if (sl.owner == &S) sl.owner = nullptr;
   }
@@ -126,8 +126,21 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
     if (int rc = svc_weights(c, S)) return rc;
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::gcm_service_kernel), c->device, cmpi::dev::kFlowLds);
   if (rc) return rc;
+  // a slot that is free (no holder, or its holder's generation has exited), starting from this
+  // service's last; else this service's own slot, whose holder is kicked
+  std::unique_lock<std::mutex> g;
+  for (int k = 0; k < kSvcSlots; ++k) {
+    const int i = (S.slot + k) % kSvcSlots;
+    std::unique_lock<std::mutex> t(svc_slot(S.dev, i).m);
+    Svc* o = svc_slot(S.dev, i).owner;
+    if (!o || o == &S || __atomic_load_n(o->done() + 12, __ATOMIC_ACQUIRE) == o->gen) {
+      S.slot = i;
+      g = std::move(t);
+      break;
+    }
+  }
+  if (!g.owns_lock()) g = std::unique_lock<std::mutex>(svc_slot(S.dev, S.slot).m);
   SvcSlot& sl = svc_slot(S.dev, S.slot);
-  std::lock_guard<std::mutex> g(sl.m);
   DeviceGuard dg(S.dev);
   if (!sl.st && lib_stream(&sl.st, true) != hipSuccess) return fail(CMPI_EHIP, "service stream creation failed");
   S.st = sl.st;
