@@ -35,6 +35,7 @@ SvcSlot& svc_slot(int dev, int i) {
   return slots[dev][i];
 }
 std::atomic<uint32_t> g_svc_next_slot[kSvcMaxDevices];
+std::atomic<int> g_svc_ls_min{0};  // cmpi_debug_set_svc_ls_min (A/B of the service's chunk length)
 
 struct Svc {
   hipStream_t st = nullptr;    // the slot's stream (shared; not owned)
@@ -158,6 +159,7 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
   a.te0 = c->dt->te0;
   a.wtab = reinterpret_cast<const cmpi::dev::u32x4*>(c->dt->fnib[0]);
   a.seq0 = seq0;
+  a.ls_min = (uint32_t)g_svc_ls_min.load();
   a.gen = ++S.gen;
   a.idle_ticks = (uint64_t)S.idle_us * 100u;
   a.life_ticks = kSvcLifeUs * 100u;

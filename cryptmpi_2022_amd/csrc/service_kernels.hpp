@@ -68,6 +68,7 @@ struct SvcArgs {
   const uint32_t* te0;
   const u32x4* wtab;     // the ten flow nibble tables (DevTables::fnib)
   uint32_t seq0;         // last seq consumed before this launch
+  uint32_t ls_min;       // smallest chunk-step exponent (test hook cmpi_debug_set_svc_ls_min; 0)
   uint32_t gen;
   uint64_t idle_ticks, life_ticks, cap_ticks;  // 100 MHz wall clock
   RoundKeys rk;
@@ -120,9 +121,9 @@ __device__ __forceinline__ uint64_t lds_ptr64(uint32_t off) {
 
 // Chunk plan of a message of `len` bytes: C = 64·2^ls X-blocks per chunk, nch chunks (chunk 0
 // takes the remainder), ngrp workgroups of 8 chunks.
-__device__ __forceinline__ uint32_t svc_plan(uint32_t len, uint32_t& ls, uint32_t& nch) {
+__device__ __forceinline__ uint32_t svc_plan(uint32_t len, uint32_t& ls, uint32_t& nch, uint32_t ls_min = 0u) {
   const uint32_t nx = ((len + 15u) >> 4) + 1u;
-  ls = 0u;
+  ls = ls_min;
   while (ls < 3u && nx >= (kSvcMaxChunks + 1u) * (64u << ls)) ++ls;
   const uint32_t C = 64u << ls;
   nch = nx >= C ? nx / C : 1u;
@@ -148,7 +149,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   a.nfix[2] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 40u));
   const uint32_t nx = a.nb + 1u;
   uint32_t ls, nch;  // chunk 0: C <= r0 < 2C (or the whole message)
-  const uint32_t ngrp = svc_plan(len, ls, nch);  // workgroups with chunks
+  const uint32_t ngrp = svc_plan(len, ls, nch, s.ls_min);  // workgroups with chunks
   const uint32_t C = 64u << ls;
   a.S = 1u << ls;
   a.nch = nch;
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
           __builtin_amdgcn_s_sleep(2);
         }
         uint32_t ls_, nch_;
-        if (!ex && d[0] <= kSvcOpen && svc_plan(d[1], ls_, nch_) > 1u) {  // seqlock: version odd while the descriptor is rewritten
+        if (!ex && d[0] <= kSvcOpen && svc_plan(d[1], ls_, nch_, s.ls_min) > 1u) {  // seqlock: version odd while the descriptor is rewritten
           wt_store(s.go + 3, ++ver);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll

@@ -42,6 +42,9 @@ void cmpi_debug_set_flow_threads(int threads);
  * predicated selects (default), 1 = branches, 0 = a store per step; 3 / 4 = the select / branch
  * form on every batch (tests). */
 void cmpi_debug_set_lane_pair(int on);
+/* resident service: smallest chunk length exponent (chunks of 64·2^ls blocks, 0..3; 0 default),
+ * taken at the service's next launch. */
+void cmpi_debug_set_svc_ls_min(int ls);
 /* FLOW kernel: a batch whose chunks all fit one workgroup finishes its tags in-kernel (1, default)
  * or through the XOR-combine launch (0). */
 void cmpi_debug_set_flow_one_wg(int on);
