@@ -28,7 +28,8 @@ struct Svc;
 struct SvcSlot {
   std::mutex m;
   hipStream_t st = nullptr;
-  Svc* owner = nullptr;  // the service whose generation was launched last on this slot
+  Svc* owner = nullptr;     // the service whose generation was launched last on this slot
+  uint32_t owner_gen = 0;   // that generation (the owner may since have moved to another slot)
 };
 SvcSlot& svc_slot(int dev, int i) {
   static SvcSlot slots[kSvcMaxDevices][kSvcSlots];
@@ -99,7 +100,11 @@ void svc_release(Svc& S) {
   if (S.go) (void)hipFree(S.go);
   if (S.wts) (void)hipFree(S.wts);
   if (S.bounce) (void)hipHostFree(S.bounce);
-  S = Svc{};
+  S.hw = nullptr;  // (the Svc is deleted by its caller)
+  S.go = nullptr;
+  S.wts = nullptr;
+  S.bounce = nullptr;
+  S.ev = nullptr;
 }
 
 // H^(1 + (63-k)·64·2^s) at wts[256s + 4k + 3] (the flow kernel's chunk-weight slot layout)
@@ -133,8 +138,9 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
   for (int k = 0; k < kSvcSlots; ++k) {
     const int i = (S.slot + k) % kSvcSlots;
     std::unique_lock<std::mutex> t(svc_slot(S.dev, i).m);
-    Svc* o = svc_slot(S.dev, i).owner;
-    if (!o || o == &S || __atomic_load_n(o->done() + 12, __ATOMIC_ACQUIRE) == o->gen) {
+    const SvcSlot& c_sl = svc_slot(S.dev, i);
+    Svc* o = c_sl.owner;
+    if (!o || o == &S || __atomic_load_n(o->done() + 12, __ATOMIC_ACQUIRE) == c_sl.owner_gen) {
       S.slot = i;
       g = std::move(t);
       break;
@@ -145,8 +151,8 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
   DeviceGuard dg(S.dev);
   if (!sl.st && lib_stream(&sl.st, true) != hipSuccess) return fail(CMPI_EHIP, "service stream creation failed");
   S.st = sl.st;
-  if (sl.owner && sl.owner != &S)  // its generation (if still resident) leaves at its next poll
-    __atomic_store_n(sl.owner->kick(), sl.owner->gen, __ATOMIC_RELEASE);
+  if (sl.owner && sl.owner != &S)  // the slot's generation (if still resident) leaves at its next poll
+    __atomic_store_n(sl.owner->kick(), sl.owner_gen, __ATOMIC_RELEASE);
   if ((rc = wait_keys(c, S.st))) return rc;  // tables of a re-key still in flight on the caller's stream
   cmpi::dev::SvcArgs a{};
   a.ring = S.dw;
@@ -171,6 +177,7 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
                           dim3(cmpi::dev::kSvcThreads), kargs, cmpi::dev::kFlowLds, S.st));
   HIP_TRY(hipEventRecord(S.ev, S.st));
   sl.owner = &S;
+  sl.owner_gen = S.gen;
   S.launched = true;
   S.running = true;
   return CMPI_OK;
