@@ -163,7 +163,7 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
   a.part = reinterpret_cast<cmpi::dev::u32x4*>(S.go + 32);
   a.wts = S.wts;
   a.te0 = c->dt->te0;
-  a.wtab = reinterpret_cast<const cmpi::dev::u32x4*>(c->dt->fnib[0]);
+  a.wtab = c->alg == CMPI_AES_128_GCM ? reinterpret_cast<const cmpi::dev::u32x4*>(c->dt->fnib[0]) : nullptr;
   a.seq0 = seq0;
   a.ls_min = (uint32_t)g_svc_ls_min.load();
   a.gen = ++S.gen;

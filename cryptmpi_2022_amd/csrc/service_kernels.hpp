@@ -66,7 +66,7 @@ struct SvcArgs {
   u32x4* part;           // device: one partial per workgroup
   const u32x4* wts;      // device: 4 x 64 x 4; wts[256s + 4k + 3] = H^(1 + (63-k)·64·2^s)
   const uint32_t* te0;
-  const u32x4* wtab;     // the ten flow nibble tables (DevTables::fnib)
+  const u32x4* wtab;     // the ten flow nibble tables (DevTables::fnib); null for CTR / ECB contexts
   uint32_t seq0;         // last seq consumed before this launch
   uint32_t ls_min;       // smallest chunk-step exponent (test hook cmpi_debug_set_svc_ls_min; 0)
   uint32_t gen;
@@ -272,11 +272,14 @@ __device__ __forceinline__ void svc_stream_op(const SvcArgs& s, const RowLanes& 
 }
 
 __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
-  {
+  if (s.wtab) {  // GCM: the AES rows and the flow kernel's ten GHASH tables
     GcmArgs t{};
     t.te0 = s.te0;
     t.wtab = s.wtab;
     stage_flow<kSvcThreads>(t);
+  } else {  // CTR / ECB contexts: the AES rows only
+    stage_rows(s.te0, kGcmRows);
+    __syncthreads();
   }
   const RowLanes rl = row_lanes(kGcmRows);
   const bool leader = blockIdx.x == 0u;
