@@ -238,6 +238,9 @@ __device__ __forceinline__ void svc_stream_op(const SvcArgs& s, const RowLanes& 
     }
   }
   const uint32_t nblk = skip ? 0u : (len + 15u) >> 4;
+  // whole blocks stored write-through (sc1, as the flow kernel's records): the release before the
+  // completion then has no dirty output lines to write back
+  const __amdgpu_buffer_rsrc_t orsrc = wt_rsrc(outp);
   for (uint32_t j = threadIdx.x; j < nblk; j += kSvcThreads) {
     const uint32_t off = 16u * j, rem = len - off < 16u ? len - off : 16u;
     u32x4 ks;
@@ -245,7 +248,7 @@ __device__ __forceinline__ void svc_stream_op(const SvcArgs& s, const RowLanes& 
       const u32x4 b = ld_blk(inp + off);
       uint32_t w0 = b[0], w1 = b[1], w2 = b[2], w3 = b[3];
       aes128_enc(s.rk, rl, w0, w1, w2, w3);
-      st_blk(outp + off, u32x4{w0, w1, w2, w3});
+      st_wt(orsrc, off, u32x4{w0, w1, w2, w3});
       continue;
     }
     if (op == kSvcXor) {
@@ -258,7 +261,7 @@ __device__ __forceinline__ void svc_stream_op(const SvcArgs& s, const RowLanes& 
     }
     u32x4 v = {0u, 0u, 0u, 0u};
     if (inp) v = rem == 16u ? ld_blk(inp + off) : load_partial(inp + off, rem);
-    if (rem == 16u) st_blk(outp + off, v ^ ks);
+    if (rem == 16u) st_wt(orsrc, off, v ^ ks);
     else store_partial(outp + off, v ^ ks, rem);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
