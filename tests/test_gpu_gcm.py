@@ -295,6 +295,9 @@ def test_flow_two_streams_one_fresh_context():
     for (n, nrec, pt, nonces, _, d_n, out), s in zip(data, streams):
         assert np.array_equal(host(out)[: nrec * (n + 16)].reshape(nrec, n + 16), oracle.gcm_seal_batch(KEY, nonces, pt))
         back, st = empty(nrec * n, fill=0xAA), status_buf(nrec)
+        # the fills run on the current stream: s waits for them, or a late fill overwrites the
+        # open's statuses / plaintext
+        s.wait_stream(torch.cuda.current_stream())
         ctx.open_batch(back, out, d_n, n, nrec, status=st, stream=s)
         outs.append((back, st))
     torch.cuda.synchronize()
