@@ -419,9 +419,11 @@ GcmPlan plan_gcm(const cmpi_ctx* c, size_t len, size_t nrec) {
     p.G = (uint32_t)(64 * S);
     p.nseg = (uint32_t)std::max<uint64_t>(1, nx / p.G);
     p.r0 = (uint32_t)(nx - (uint64_t)(p.nseg - 1) * p.G);
-    // few waves (single messages, the 600/EVP regime; the naive alltoall's 8 x 1 MiB): 512-thread
-    // workgroups (1 x 64 KiB seal 21.0 -> 15.7 us at S = 2)
-    if ((uint64_t)nrec * p.nseg <= (uint64_t)c->ncu * 8) p.nt = 512;
+    // 512-thread workgroups: few waves (single messages, the 600/EVP regime; the naive
+    // alltoall's 8 x 1 MiB: 1 x 64 KiB seal 21.0 -> 15.7 us at S = 2) and several rounds alike
+    // (the 1024-thread form is capped at 128 VGPRs and spills: 3000 / 4096 / 6000 x 1 KiB seal
+    // 25.0 / 25.8 / 38.4 -> 23.7 / 24.2 / 32.3 us, profiles/r04zzb_nt_ab.txt)
+    p.nt = 512;
     if (fnt) p.nt = (uint32_t)fnt;
     return p;
   }

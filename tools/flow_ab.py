@@ -23,7 +23,8 @@ SHAPES = {"8x1MiB": (1 << 20, 8), "1x64KiB": (65536, 1), "3x100000": (100000, 3)
           "32x256KiB": (256 << 10, 32), "8x(1MiB-5)": ((1 << 20) - 5, 8), "65536x1000": (1000, 65536),
           "1x1000": (1000, 1), "64x1000": (1000, 64), "2048x1000": (1000, 2048), "16x100": (100, 16),
           "1x100": (100, 1), "2048x600": (600, 2048), "2048x300": (300, 2048), "2048x200": (200, 2048),
-          "256x260": (260, 256), "16x300": (300, 16), "65536x1024": (1024, 65536), "65536x4096": (4096, 65536)}
+          "256x260": (260, 256), "16x300": (300, 16), "65536x1024": (1024, 65536), "65536x4096": (4096, 65536),
+          "3000x1024": (1024, 3000), "4096x1024": (1024, 4096), "6000x1024": (1024, 6000), "2500x4000": (4000, 2500)}
 
 
 def shapes() -> dict:
