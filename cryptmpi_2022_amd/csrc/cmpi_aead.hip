@@ -21,6 +21,8 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include <sys/random.h>
@@ -59,6 +61,23 @@ int fail(int code, const char* fmt, ...) {
     hipError_t e_ = (expr);                                                              \
     if (e_ != hipSuccess) return fail(CMPI_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
+
+// Kernel launch that reports its own status: hipGetLastError() after a triple-chevron
+// or hipLaunchKernelGGL launch returns the thread's last error from ANY earlier HIP call — the
+// caller's included — and clears it, so an unrelated earlier failure would fail the seal (and the
+// EVP shim put zeros on the wire) while the caller lost its own error.  hipLaunchKernel returns
+// the launch's status and leaves a pending error of the caller's alone.
+template <class... P, class... A>
+hipError_t launch_k(void (*fn)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t st, A&&... a) {
+  static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+  std::tuple<std::decay_t<P>...> t(std::forward<A>(a)...);
+  return std::apply(
+      [&](auto&... x) {
+        void* args[] = {static_cast<void*>(&x)...};
+        return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, block, args, lds, st);
+      },
+      t);
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -523,18 +542,16 @@ int get_chw(const cmpi_ctx* c, uint32_t C, uint32_t nch, const u32x4** out, hipS
 template <bool DEC>
 int launch_gcm_combine(const cmpi_ctx* c, cmpi::dev::GcmCombineArgs& ca, uint32_t G, hipStream_t st) {
   if (ca.prew && !ca.ekj0) {  // partials already weighted, E_K(J0) inside: XOR only
-    hipLaunchKernelGGL(cmpi::dev::gcm_xor_combine_kernel<DEC>, dim3(ca.nrec), dim3(cmpi::dev::kXorCombineThreads), 128,
-                       st, ca);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_k(cmpi::dev::gcm_xor_combine_kernel<DEC>, dim3(ca.nrec), dim3(cmpi::dev::kXorCombineThreads), 128,
+                       st, ca));
     return CMPI_OK;
   }
   int rc = get_mj(c, G, ca);
   if (rc) return rc;
   const uint32_t wpb = cmpi::dev::kCombineThreads / 64u;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((ca.nrec + wpb - 1u) / wpb, 2u * (uint32_t)c->ncu));
-  hipLaunchKernelGGL(cmpi::dev::gcm_combine_kernel<DEC>, dim3(grid), dim3(cmpi::dev::kCombineThreads),
-                     cmpi::dev::kCombineLds, st, ca);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(cmpi::dev::gcm_combine_kernel<DEC>, dim3(grid), dim3(cmpi::dev::kCombineThreads),
+                     cmpi::dev::kCombineLds, st, ca));
   return CMPI_OK;
 }
 
@@ -555,8 +572,7 @@ int launch_gcm_main(const cmpi::dev::GcmArgs& a, int device, uint32_t grid, size
                       : cmpi::dev::gcm_lane_kernel<L, DEC, 0>;
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), device, lds);
   if (rc) return rc;
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(kGcmThreads), lds, st, a);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(fn, dim3(grid), dim3(kGcmThreads), lds, st, a));
   return CMPI_OK;
 }
 
@@ -783,8 +799,7 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   if (rc) return rc;
   const uint64_t waves = a.nitems;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + 15) / 16, (uint64_t)c->ncu * per_cu));
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(1024), lds, st, a);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(fn, dim3(grid), dim3(1024), lds, st, a));
 
   cmpi::dev::OcbFinalArgs f{};
   f.in = in;
@@ -807,9 +822,8 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     int rc1 = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ocb_final_kernel<DEC>), c->device, cmpi::dev::kOcbFinalLds);
     if (rc1) return rc1;
   }
-  hipLaunchKernelGGL(cmpi::dev::ocb_final_kernel<DEC>, dim3((uint32_t)((nrec + 255) / 256)), dim3(256),
-                     cmpi::dev::kOcbFinalLds, st, f);  // open: verdicts and the zero-fill of forged records
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(cmpi::dev::ocb_final_kernel<DEC>, dim3((uint32_t)((nrec + 255) / 256)), dim3(256),
+                     cmpi::dev::kOcbFinalLds, st, f));  // open: verdicts and the zero-fill of forged records
   return CMPI_OK;
 }
 
@@ -826,12 +840,20 @@ std::atomic<size_t> g_host_chunk{(size_t)16 << 20};  // 8 / 16 / 32 MiB: 30.1 / 
 // direct source/target of an asynchronous DMA.  Pageable memory is never handed to async copies
 // (the runtime's pageable path under concurrent streams faulted in testing, round 1): it goes
 // through our pinned staging slots with a CPU pack/unpack overlapped with the other chunks.
+//
+// hipPointerGetAttributes fails (hipErrorInvalidValue) on pageable memory and records that as the
+// thread's last error; ptr_attrs clears the failure it caused only when no error of the caller's
+// was pending before the query, so a caller's error stays readable.
+bool ptr_attrs(const void* p, hipPointerAttribute_t* at) {
+  const hipError_t prior = hipPeekAtLastError();
+  if (hipPointerGetAttributes(at, p) == hipSuccess) return true;
+  if (prior == hipSuccess) (void)hipGetLastError();
+  return false;
+}
+
 bool is_pinned(const void* p) {
   hipPointerAttribute_t at;
-  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
+  if (!ptr_attrs(p, &at)) return false;
   return at.type == hipMemoryTypeHost;
 }
 
@@ -868,10 +890,7 @@ void par_copy_records(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t sp
 // Device address of page-locked host memory (the kernel reads / writes it over PCIe), or null.
 void* pinned_dev_ptr(const void* p) {
   hipPointerAttribute_t at;
-  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
+  if (!ptr_attrs(p, &at)) return nullptr;
   if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
   const uintptr_t off = at.hostPointer ? (uintptr_t)p - (uintptr_t)at.hostPointer : 0;
   return (uint8_t*)at.devicePointer + off;
@@ -914,8 +933,7 @@ hipError_t flag_wait(HostPipe& P, hipStream_t st) {
   if (mode == 1) {
     e = hipStreamWriteValue32(st, P.dflag, seq, 0);
   } else {
-    done_flag_kernel<<<1, 64, 0, st>>>(P.dflag, seq);
-    e = hipGetLastError();
+    e = launch_k(done_flag_kernel, dim3(1), dim3(64), 0, st, P.dflag, seq);
   }
   if (e != hipSuccess) return e;
   const auto t0 = std::chrono::steady_clock::now();
@@ -1201,8 +1219,7 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   const int lds = 65536;
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds);
   if (rc) return rc;
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(1024), lds, st, a);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(fn, dim3(grid), dim3(1024), lds, st, a));
   return CMPI_OK;
 }
 
@@ -1496,8 +1513,7 @@ int cmpi_gcm_seal_batch_fresh(const cmpi_ctx* c, uint8_t* out, size_t out_stride
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::nonce_drbg_kernel), c->device, 65536);
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nrec + 1023) / 1024, (uint64_t)c->ncu));
-  hipLaunchKernelGGL(cmpi::dev::nonce_drbg_kernel, dim3(grid), dim3(1024), 65536, (hipStream_t)stream, na);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(cmpi::dev::nonce_drbg_kernel, dim3(grid), dim3(1024), 65536, (hipStream_t)stream, na));
   return gcm_batch<false>(c, out, out_stride, in, in_stride, nonce_out, nonce_stride, len, nrec, nullptr, workspace,
                           stream);
 }
@@ -1627,8 +1643,7 @@ int cmpi_ecb_encrypt(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t 
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 1023) / 1024, (uint64_t)c->ncu * 2));
   int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::ecb_kernel), c->device, 65536);
   if (rc) return rc;
-  hipLaunchKernelGGL(cmpi::dev::ecb_kernel, dim3(grid), dim3(1024), 65536, (hipStream_t)stream, a);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(cmpi::dev::ecb_kernel, dim3(grid), dim3(1024), 65536, (hipStream_t)stream, a));
   return CMPI_OK;
 }
 
@@ -1674,11 +1689,9 @@ int cmpi_ctx_rekey_subkey(cmpi_ctx* dst, const cmpi_ctx* base, const uint8_t v[1
     memset(&dst->drk, 0, sizeof dst->drk);
     memset(&dst->H, 0, sizeof dst->H);
   }
-  hipLaunchKernelGGL(cmpi::dev::gcm_keysetup_kernel, dim3(1), dim3(256), cmpi::dev::kKsLds, (hipStream_t)stream, a);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(cmpi::dev::gcm_tables_kernel, dim3((cmpi::dev::kTabEntries + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, ta);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(cmpi::dev::gcm_keysetup_kernel, dim3(1), dim3(256), cmpi::dev::kKsLds, (hipStream_t)stream, a));
+  HIP_TRY(launch_k(cmpi::dev::gcm_tables_kernel, dim3((cmpi::dev::kTabEntries + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, ta));
   return record_keys(dst, (hipStream_t)stream);
 }
 
@@ -1726,11 +1739,9 @@ int cmpi_ctx_rekey(cmpi_ctx* c, const uint8_t* key, size_t key_len, void* stream
   cmpi::aes128_encrypt_words_host(c->rk.w, z, h);
   memcpy(c->H.b, h, 16);
   c->dev_keys = false;
-  hipLaunchKernelGGL(cmpi::dev::gcm_keysetup_kernel, dim3(1), dim3(256), cmpi::dev::kKsLds, (hipStream_t)stream, a);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(cmpi::dev::gcm_tables_kernel, dim3((cmpi::dev::kTabEntries + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, ta);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(cmpi::dev::gcm_keysetup_kernel, dim3(1), dim3(256), cmpi::dev::kKsLds, (hipStream_t)stream, a));
+  HIP_TRY(launch_k(cmpi::dev::gcm_tables_kernel, dim3((cmpi::dev::kTabEntries + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, ta));
   if (c->alg == CMPI_AES_128_OCB) {  // RFC 7253 L table from L_* = E_K(0) (host, 1 KiB)
     uint8_t lt[66][16];
     memcpy(lt[0], c->H.b, 16);
@@ -1770,8 +1781,8 @@ cmpi_ctx* cmpi_ctx_new_subkey(const cmpi_ctx* base, const uint8_t v[16]) {
   cmpi_ctx* c = cmpi_ctx_derive_subkey(base, v, nullptr);
   if (!c) return nullptr;
   DeviceGuard dg(c->device);
-  if (hipStreamSynchronize(nullptr) != hipSuccess) {
-    fail(CMPI_EHIP, "key setup failed: %s", hipGetErrorString(hipGetLastError()));
+  if (const hipError_t e = hipStreamSynchronize(nullptr); e != hipSuccess) {
+    fail(CMPI_EHIP, "key setup failed: %s", hipGetErrorString(e));
     cmpi_ctx_free(c);
     return nullptr;
   }

@@ -30,8 +30,7 @@ int xor_launch(uint8_t* out, const uint8_t* a, const uint8_t* b, size_t n, hipSt
   if (n == 0) return CMPI_OK;
   const uint64_t nv = n / 16;
   const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((nv + 255) / 256, 4096));
-  hipLaunchKernelGGL(cmpi::dev::xor_bytes_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, out, a, b, (uint64_t)n);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launch_k(cmpi::dev::xor_bytes_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, out, a, b, (uint64_t)n));
   return CMPI_OK;
 }
 
@@ -75,9 +74,16 @@ struct Served {
 
 // Ring operations chain on r->last (called with r->mu held): the launch stream waits for the
 // previous operation when it ran on another stream, and records the new last use after.
+// Constructed in place and never copied (a copied temporary's destructor marked the
+// new stream as the ring's last one before begin() ran, so the cross-stream wait was skipped);
+// the ring's last use moves to `st` only once begin() has ordered the stream.
 struct RingOrder {
   cmpi_ctr_ring* r;
   hipStream_t st;
+  bool armed = false;
+  RingOrder(cmpi_ctr_ring* r_, hipStream_t st_) : r(r_), st(st_) {}
+  RingOrder(const RingOrder&) = delete;
+  RingOrder& operator=(const RingOrder&) = delete;
   int begin() {
     if (r->used && r->last_stream != st) {
       if (r->pending) {
@@ -86,9 +92,11 @@ struct RingOrder {
       }
       HIP_TRY(hipStreamWaitEvent(st, r->last, 0));
     }
+    armed = true;
     return CMPI_OK;
   }
   ~RingOrder() {
+    if (!armed) return;
     r->used = true;
     r->last_stream = st;
     r->pending = true;
@@ -149,8 +157,19 @@ void cmpi_ctr_ring_free(cmpi_ctr_ring* r) {
   if (!r) return;
   DeviceGuard dg(r->ctx->device);
   if (r->used) {  // the ring's last fill / consumption
-    if (r->pending) (void)hipEventRecord(r->last, r->last_stream);
-    (void)hipEventSynchronize(r->last);
+    bool drained = false;
+    if (r->pending) {
+      // if the record fails (the last op's stream is gone), the ring must still not be
+      // freed under its last use — drain the device instead (free is rare; no error is left behind
+      // unless the caller already had one pending)
+      const hipError_t prior = hipPeekAtLastError();
+      if (hipEventRecord(r->last, r->last_stream) != hipSuccess) {
+        if (prior == hipSuccess) (void)hipGetLastError();
+        (void)hipDeviceSynchronize();
+        drained = true;
+      }
+    }
+    if (!drained) (void)hipEventSynchronize(r->last);
   }
   if (r->last) (void)hipEventDestroy(r->last);
   if (r->dring) (void)hipFree(r->dring);
@@ -177,7 +196,7 @@ int cmpi_ctr_ring_generate(cmpi_ctr_ring* r, size_t gen_bytes, void* stream) {
   DeviceGuard dg(r->ctx->device);
   const int gen = (int)gen_bytes;
   if (!(r->compute_size <= (r->max - gen - 1024))) return 0;
-  RingOrder ord{r, (hipStream_t)stream};
+  RingOrder ord(r, (hipStream_t)stream);
   if (int e = ord.begin()) return e;
   int blockamount = ((gen - 1) / 16) * 16 + 16;
   int rc;
@@ -225,7 +244,7 @@ int ring_encrypt_locked(cmpi_ctr_ring* r, uint8_t* out, const uint8_t* in, size_
   if (sv) {
     if (int e = ring_drain(r)) return e;
   } else {
-    ord.emplace(RingOrder{r, st});
+    ord.emplace(r, st);
     if (int e = ord->begin()) return e;
   }
   auto xor_op = [&](uint8_t* o, const uint8_t* m, const uint8_t* i, size_t len) {

@@ -6,11 +6,29 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dlfcn.h>
 
 #include "../include/cmpi_evp.h"
 
+/* CMPI_TEST_PROVOKE_HIP_ERROR (tests/test_gpu_errors.py): a HIP error of the caller's own is left
+ * pending in this thread before the first EVP call; after the last one it must still be pending
+ * (the drop-in reports only errors its own calls cause, and never clears the caller's). */
+typedef int (*hip_int_fn)(int);
+typedef int (*hip_void_fn)(void);
+static int provoked = 0;
+static hip_void_fn peek_last = 0;
+
 int main(int argc, char **argv) {
   if (argc != 5) return 2;
+  if (getenv("CMPI_TEST_PROVOKE_HIP_ERROR")) {
+    void *h = dlopen("libamdhip64.so.7", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return 13;
+    hip_int_fn set_device = (hip_int_fn)dlsym(h, "hipSetDevice");
+    peek_last = (hip_void_fn)dlsym(h, "hipPeekAtLastError");
+    if (!set_device || !peek_last) return 13;
+    provoked = set_device(9999);
+    if (provoked == 0 || peek_last() != provoked) return 13;
+  }
   int p = atoi(argv[1]);          /* peers */
   unsigned long n = strtoul(argv[2], 0, 10); /* bytes per peer block */
   FILE *f = fopen(argv[3], "rb");
@@ -72,5 +90,13 @@ int main(int argc, char **argv) {
   EVP_AEAD_CTX_free(ctx);
   EVP_CIPHER_CTX_free(ctx_enc);
   EVP_CIPHER_CTX_free(cctx);
+  if (provoked) {
+    const int now = peek_last();
+    if (now != provoked) {
+      fprintf(stderr, "caller HIP error %d replaced by %d\n", provoked, now);
+      return 12;
+    }
+    fprintf(stderr, "caller error preserved (%d)\n", now);
+  }
   return 0;
 }

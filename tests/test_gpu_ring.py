@@ -91,3 +91,28 @@ def test_sender_ring_receiver_mask_round_trip(ctx):
     ring.mask_decrypt(ctx, out, ct, n, mask, 10016, iv, 626)  # 10016/16 blocks from the ring
     assert host(out)[:n].tobytes() == pt.tobytes()
     assert g.state()["counter_needto_send"] == (n + 15) // 16
+
+
+@pytest.mark.parametrize("rounds", [1, 3])
+def test_ring_fill_and_encrypt_on_two_streams(rounds, ctx):
+    """the ring is filled on stream B behind ~10 ms of queued GPU work and the
+    XOR that consumes it runs on stream A; the XOR must wait for the fill (RingOrder is built in
+    place, so the cross-stream wait is not skipped) and the bytes must match the oracle."""
+    import torch
+
+    iv = splitmix64_bytes(0x2B, 16).tobytes()
+    g = ring.CtrRing(ctx, iv, 65536)
+    o = oracle.Ring(KEY, iv, 65536)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for r in range(rounds):
+        n = 4096 + 16 * r
+        pt = splitmix64_bytes(0x2C + r, n)
+        inp, out = dev(pt), empty(n, fill=0)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(sb):
+            torch.cuda._sleep(20_000_000)  # long work ahead of the fill on stream B
+        assert g.generate(n, stream=sb) == o.generate(n)
+        g.encrypt(out, inp, n, stream=sa)
+        torch.cuda.synchronize()
+        assert host(out)[:n].tobytes() == o.encrypt(pt.tobytes()), r
+        assert g.state() == o.state(), r
