@@ -40,6 +40,10 @@ WORKLOADS = {
     "gcm4k": ("gcm", 4096, 65536, "north-star target: 65536 x 4 KiB AES-128-GCM seal+open"),
     "ocb1m": ("ocb", 1 << 20, 4096, "BASELINE config 3: 4096 x 1 MiB AES-128-OCB seal+open"),
     "ctr1g": ("ctr", 1 << 30, 1, "BASELINE config 4: 1 GiB AES-128-CTR keystream+XOR"),
+    # SURVEY §8(d) config 4's second form: the keystream materialised into a 1 GiB mask (the a8
+    # mask ring, generateCommonEncMask send.c:1162-1266) and then XORed with the payload
+    # (encryption_common_counter send.c:1273-1465) — two kernels, 4n algorithmic bytes
+    "ctr1g_mask": ("ctrmask", 1 << 30, 1, "BASELINE config 4, materialised mask: 1 GiB keystream, then XOR"),
     "alltoall": ("gcm", 1 << 20, 8, "BASELINE config 5 per rank: 8 peers x 1 MiB seal+open"),
 }
 
@@ -61,9 +65,10 @@ class Workload:
         g = torch.Generator(device=self.dev).manual_seed(seed)
         n, N = self.n, self.nrec
         self.pt = torch.randint(0, 256, (N * n,), dtype=torch.uint8, device=self.dev, generator=g)
-        if self.alg == "ctr":
+        if self.alg in ("ctr", "ctrmask"):
             self.ctx = aead.CipherCtx(KEY, "aes-128-ctr", device=device)
             self.ct = torch.empty_like(self.pt)
+            self.mask = torch.empty_like(self.pt) if self.alg == "ctrmask" else None
             self.ctr0 = bytes(range(0xF0, 0x100))
             self.pt_sample = self.pt[: 1 << 24].clone()  # open writes the plaintext back in place
             self._bind()
@@ -77,10 +82,13 @@ class Workload:
         self.ws = torch.empty(max(ws, 16), dtype=torch.uint8, device=self.dev) if ws else None
         self._bind()
 
-    # algorithmic HBM bytes per launch: seal/open 2n+28 per record, CTR fused 2n
+    # algorithmic HBM bytes per launch: seal/open 2n+28 per record, CTR fused 2n,
+    # CTR with a materialised mask 4n (write mask; read mask + payload, write ct)
     def bytes_per_launch(self) -> int:
         if self.alg == "ctr":
             return 2 * self.n
+        if self.alg == "ctrmask":
+            return 4 * self.n
         return self.nrec * (2 * self.n + 28)
 
     def _bind(self):
@@ -97,6 +105,12 @@ class Workload:
             self._seal_call = (L.cmpi_ctr_xor, (h, P(self.ct), P(self.pt), self.n, cb, st))
             self._open_call = (L.cmpi_ctr_xor, (h, P(self.pt), P(self.ct), self.n, cb, st))
             return
+        if self.alg == "ctrmask":  # mask = E_K(ctr0 + i) (cmpi_ctr_keystream), then out = in ^ mask
+            cb = (ctypes.c_uint8 * 16).from_buffer_copy(self.ctr0)
+            ks = (L.cmpi_ctr_keystream, (h, P(self.mask), self.n // 16, cb, st))
+            self._seal_call = [ks, (L.cmpi_xor_bytes, (P(self.ct), P(self.pt), P(self.mask), self.n, st))]
+            self._open_call = [ks, (L.cmpi_xor_bytes, (P(self.pt), P(self.ct), P(self.mask), self.n, st))]
+            return
         n, N_ = self.n, self.nrec
         seal = L.cmpi_gcm_seal_batch if self.alg == "gcm" else L.cmpi_ocb_seal_batch
         opn = L.cmpi_gcm_open_batch if self.alg == "gcm" else L.cmpi_ocb_open_batch
@@ -104,25 +118,24 @@ class Workload:
         self._open_call = (opn, (h, P(self.back), n, P(self.ct), n + 16, P(self.nonces), 12, n, N_, P(self.status),
                                  P(self.ws), st))
 
-    def seal(self):
-        fn, args = self._seal_call
-        rc = fn(*args)
-        if rc:
-            from cryptmpi_2022_amd import _native as N
+    @staticmethod
+    def _run(calls):
+        for fn, args in calls if isinstance(calls, list) else [calls]:
+            rc = fn(*args)
+            if rc:
+                from cryptmpi_2022_amd import _native as N
 
-            N.check(rc)
+                N.check(rc)
+
+    def seal(self):
+        self._run(self._seal_call)
 
     def open(self):
-        fn, args = self._open_call
-        rc = fn(*args)
-        if rc:
-            from cryptmpi_2022_amd import _native as N
-
-            N.check(rc)
+        self._run(self._open_call)
 
     def verify(self) -> bool:
         torch.cuda.synchronize(self.dev)
-        if self.alg == "ctr":  # ct != pt, and decrypting ct in place restored the plaintext
+        if self.alg in ("ctr", "ctrmask"):  # ct != pt, and decrypting ct in place restored the plaintext
             return (not torch.equal(self.ct[: 1 << 24], self.pt_sample)) and torch.equal(self.pt[: 1 << 24], self.pt_sample)
         return bool((self.status == 1).all()) and torch.equal(self.back, self.pt)
 
@@ -141,7 +154,7 @@ class Workload:
 
     def free(self):
         self.ctx.close()
-        for a in ("_seal_call", "_open_call", "pt", "pt_sample", "ct", "back", "nonces", "status", "ws"):
+        for a in ("_seal_call", "_open_call", "pt", "pt_sample", "ct", "back", "nonces", "status", "ws", "mask"):
             if hasattr(self, a):
                 delattr(self, a)
         torch.cuda.empty_cache()
@@ -216,7 +229,7 @@ def parity_cpu(w) -> dict:
     ref = OpenSSLRef()
     torch.cuda.synchronize(w.dev)
     n, N = w.n, w.nrec
-    if w.alg == "ctr":
+    if w.alg in ("ctr", "ctrmask"):
         windows = {}
         span = 1 << 24  # 16 MiB windows
         lo = int.from_bytes(w.ctr0[12:], "big")
@@ -436,20 +449,32 @@ def lds_roofline(w, kern_ms: float, device: int) -> dict:
 
 
 def copy_peak_gbs(device: int, nbytes: int = 1 << 30, reps: int = 10) -> float:
-    """Achievable HBM bandwidth on this box: device-to-device copy of 1 GiB (read + write bytes
-    / time, best of `reps`) — the 'measured copy-kernel peak' of BASELINE.md §3."""
+    """Achievable HBM bandwidth on this box: device-to-device copy of 1 GiB by the library's
+    streaming copy kernel (cmpi_debug_copy: 16 B per lane, four loads in flight, non-temporal;
+    the guide's float4 copy measures 6.29 TB/s) — read + write bytes / time, best of `reps` —
+    the 'measured copy-kernel peak' of BASELINE.md §3.  (Round 4 timed a torch uint8 copy_,
+    4.9 TB/s, which overstated frac_measured.)"""
+    from cryptmpi_2022_amd import _native as N
+
     src = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", device))
     dst = torch.empty_like(src)
-    dst.copy_(src)
+    st = torch.cuda.current_stream(device).cuda_stream
+    lib = N.lib()
+
+    def copy():
+        N.check(lib.cmpi_debug_copy(dst.data_ptr(), src.data_ptr(), nbytes, st))
+
+    copy()
     torch.cuda.synchronize(device)
     best = float("inf")
+    ev = KernelEvents(2)
     for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        dst.copy_(src)
-        e1.record()
+        ev.record(0, st)
+        copy()
+        ev.record(1, st)
         torch.cuda.synchronize(device)
-        best = min(best, e0.elapsed_time(e1) * 1e-3)
+        best = min(best, ev.ms(0, 1) * 1e-3)
+    ev.free()
     del src, dst
     torch.cuda.empty_cache()
     return 2 * nbytes / best / 1e9
@@ -1380,7 +1405,7 @@ def main() -> None:
             result["cpu_baseline_port"] = {"error": repr(e)}
     if rank == 0 and ws == 1 and not args.no_extras and args.workload == "gcm1k":
         extras = {}
-        for name in ("gcm4k", "ocb1m", "ctr1g", "alltoall"):
+        for name in ("gcm4k", "ocb1m", "ctr1g", "ctr1g_mask", "alltoall"):
             try:
                 we = Workload(name, local, seed=77)
                 wl, s_ms, o_ms = time_steps(we, EXTRA_STEPS, EXTRA_WARMUP, barrier, warmup_s=0.3)

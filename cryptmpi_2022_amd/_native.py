@@ -133,6 +133,7 @@ _SIGS = {
     "cmpi_debug_set_host_direct": ([_S], None),
     "cmpi_debug_set_host_spin": ([_I], None),
     "cmpi_debug_event_new": ([], _P),
+    "cmpi_debug_copy": ([_P, _P, _S, _P], _I),
     "cmpi_debug_event_record": ([_P, _P], _I),
     "cmpi_debug_event_ms": ([_P, _P], ctypes.c_float),
     "cmpi_debug_event_free": ([_P], None),

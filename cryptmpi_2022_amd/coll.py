@@ -2,7 +2,8 @@
 Reference: MPIR_Naive_Sec_Alltoall (MV/src/mpi/coll/alltoall.c:764-836), MPIR_Naive_Sec_Allgather
 (allgather.c:839-899), gather 301 (gather.c:1508-1606), MPIR_Naive_Sec_Scatter (scatter.c:659-730),
 MPI_Naive_Sec_Bcast (bcast.c:1510-1580).  Wire block = nonce(12) || ct(n) || tag(16); every block
-is sealed under a fresh nonce (the reference's RAND_bytes, here the context's device DRBG).
+is sealed under a fresh nonce (the reference's RAND_bytes; here made by the seal kernel itself:
+cmpi_coll.h, a random 4-byte field and a 64-bit counter with a random start per context).
 
 The stock collective in between runs on the ciphertext through torch.distributed: RCCL over
 xGMI for device buffers (backend "nccl"), or the host transport (backend "gloo": wire blocks are

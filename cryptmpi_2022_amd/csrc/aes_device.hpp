@@ -70,6 +70,20 @@ struct RoundKeys {
   uint32_t w[44];
 };
 
+// Issue grouping of LDS lookups (CMPI_LDS_BATCH): a scheduling fence after a round's 16
+// independent table reads keeps hipcc from interleaving them with the XORs that consume them
+// (its register-pressure schedule waited for the LDS after every second read, i.e. ~70 serial
+// LDS round trips per AES block).
+#ifndef CMPI_LDS_BATCH
+#define CMPI_LDS_BATCH 0
+#endif
+__device__ __forceinline__ void lds_batch_fence() {
+  if constexpr (CMPI_LDS_BATCH & 1) __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void ghash_batch_fence() {
+  if constexpr (CMPI_LDS_BATCH & 2) __builtin_amdgcn_sched_barrier(0);
+}
+
 // Folded round keys.  A round column is T0[a] ^ T1[b] ^ K ^ rotl16(T0[c] ^ T1[d]); written as
 // xor3(T0[a], T1[b], rotl16(xor3(T0[c], T1[d], rotl16(K)))) it is 3 VALU instead of 4 (rotl16
 // is an involution).  The wave-uniform rotl16(K) of rounds 1..9 (words 4..39) is computed once
@@ -100,6 +114,7 @@ __device__ __forceinline__ void enc_round(const RowLanes& L, uint32_t& s0, uint3
   const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l1, L.m)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l1));
   const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l1, L.m)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l1));
   const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l1, L.m)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l1));
+  lds_batch_fence();
   s0 = xor3(a0, a1, rotl16(xor3(a2, a3, k0)));
   s1 = xor3(b0, b1, rotl16(xor3(b2, b3, k1)));
   s2 = xor3(c0, c1, rotl16(xor3(c2, c3, k2)));
@@ -113,6 +128,7 @@ __device__ __forceinline__ void enc_last(const RowLanes& L, uint32_t& s0, uint32
   const uint32_t b0 = lds32(ra<0>(s1, L.l0)), b1 = lds32(ra<1>(s2, L.l0, L.m)), b2 = lds32(ra<2>(s3, L.l0)), b3 = lds32(ra<3>(s0, L.l0));
   const uint32_t c0 = lds32(ra<0>(s2, L.l0)), c1 = lds32(ra<1>(s3, L.l0, L.m)), c2 = lds32(ra<2>(s0, L.l0)), c3 = lds32(ra<3>(s1, L.l0));
   const uint32_t d0 = lds32(ra<0>(s3, L.l0)), d1 = lds32(ra<1>(s0, L.l0, L.m)), d2 = lds32(ra<2>(s1, L.l0)), d3 = lds32(ra<3>(s2, L.l0));
+  lds_batch_fence();
   s0 = xor3(perm(a1, a0, 0x0c0c0501u), perm(a3, a2, 0x05010c0cu), k0);
   s1 = xor3(perm(b1, b0, 0x0c0c0501u), perm(b3, b2, 0x05010c0cu), k1);
   s2 = xor3(perm(c1, c0, 0x0c0c0501u), perm(c3, c2, 0x05010c0cu), k2);
@@ -307,6 +323,22 @@ __device__ __forceinline__ u32x4 gmul_byte(u32x4 x, const GhashLane& g, u32x4 y 
   const uint32_t z0 = g.q1 ? y1 : y0, z1 = g.q1 ? y2 : y1, z2 = g.q1 ? y3 : y2, z3 = g.q1 ? y0 : y3;
   const uint32_t w[4] = {g.q2 ? z2 : z0, g.q2 ? z3 : z1, g.q2 ? z0 : z2, g.q2 ? z1 : z3};
   u32x4 r = y;
+  if constexpr (CMPI_LDS_BATCH & 2) {  // four reads in flight per wait
+#pragma unroll
+    for (int t = 0; t < 16; t += 4) {
+      u32x4 e[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = t + i;
+        const uint32_t sel = 0x0c0c0000u | ((4u + (p & 3)) << 8) | (uint32_t)(p & 3);
+        e[i] = lds128(perm(w[p >> 2], g.po[p >> 2], sel));
+      }
+      ghash_batch_fence();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) r[c] = xor3(r[c], e[0][c], e[1][c]) ^ (e[2][c] ^ e[3][c]);
+    }
+    return r;
+  }
 #pragma unroll
   for (int t = 0; t < 16; t += 2) {
     const uint32_t sa = 0x0c0c0000u | ((4u + (t & 3)) << 8) | (uint32_t)(t & 3);

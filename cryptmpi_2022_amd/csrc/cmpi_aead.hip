@@ -151,8 +151,8 @@ struct cmpi_ctx {
   int ncu = 256;
   uint8_t key[16];
   std::atomic<bool> dev_keys{false};  // key, rk, drk and H exist only on the device (derived 602 sub-key)
-  cmpi::dev::RoundKeys nrk{};        // nonce DRBG key Kn (OS CSPRNG), cmpi_gcm_seal_batch_fresh
-  std::atomic<uint64_t> nctr{0};     // nonce DRBG counter
+  uint32_t nprefix = 0;              // fresh nonces (cmpi_gcm_seal_batch_fresh): 4 random bytes
+  std::atomic<uint64_t> nctr{0};     // and a 64-bit counter that starts at a random value
   cmpi::dev::RoundKeys rk{};
   cmpi::dev::RoundKeys drk{};
   Blk H{};
@@ -1296,7 +1296,10 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
       }
       got += (size_t)r;
     }
-    cmpi::aes128_expand_words(kn, c->nrk.w);
+    uint64_t c0;
+    memcpy(&c->nprefix, kn, 4);
+    memcpy(&c0, kn + 4, 8);
+    c->nctr.store(c0);
     memset(kn, 0, sizeof kn);
   }
   uint32_t z[4] = {0, 0, 0, 0}, h[4];
@@ -1441,6 +1444,20 @@ void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 |
 // Timing events without the system-scope release fence (hipEventDisableSystemFence): a default
 // event's fence writes back and invalidates the caches and leaves a ~6 us bubble before the
 // next launch — the bench times kernels with these instead.
+int cmpi_debug_copy(void* dst, const void* src, size_t n, void* stream) {
+  if (!dst || !src || n % 64 || ((uintptr_t)dst | (uintptr_t)src) % 16) return fail(CMPI_EINVAL, "copy: n % 64 / alignment");
+  if (n == 0) return CMPI_OK;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  int ncu = 256;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+  const uint64_t nv = n / 16u;
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((nv / 4u + 255u) / 256u, (uint64_t)ncu * 16u));
+  HIP_TRY(launch_k(cmpi::dev::copy16_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
+                   reinterpret_cast<u32x4*>(dst), reinterpret_cast<const u32x4*>(src), nv));
+  return CMPI_OK;
+}
+
 void* cmpi_debug_event_new(void) {
   hipEvent_t e = nullptr;
   if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
@@ -1502,20 +1519,16 @@ int cmpi_gcm_seal_batch_fresh(const cmpi_ctx* c, uint8_t* out, size_t out_stride
   if (nrec == 0) return CMPI_OK;
   if (!nonce_out) return fail(CMPI_EINVAL, "null nonce_out");
   if (nrec > 1 && nonce_stride < 12) return fail(CMPI_EINVAL, "nonce_stride < 12");
-  DeviceGuard dg(c->device);
-  cmpi::dev::NonceArgs na{};
-  na.out = nonce_out;
-  na.stride = nonce_stride;
-  na.nrec = nrec;
-  na.base = const_cast<cmpi_ctx*>(c)->nctr.fetch_add(nrec);
-  na.te0 = c->dt->te0;
-  na.rk = folded(c->nrk);
-  int rc = set_lds_attr(reinterpret_cast<const void*>(cmpi::dev::nonce_drbg_kernel), c->device, 65536);
-  if (rc) return rc;
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nrec + 1023) / 1024, (uint64_t)c->ncu));
-  HIP_TRY(launch_k(cmpi::dev::nonce_drbg_kernel, dim3(grid), dim3(1024), 65536, (hipStream_t)stream, na));
+  // nonce_r = prefix || BE64(base + r): the seal kernel makes and writes them itself (one launch,
+  // where round 4 ran a DRBG kernel first: 4.6 us per naive-collective seal)
+  const uint64_t base = const_cast<cmpi_ctx*>(c)->nctr.fetch_add(nrec);
+  NonceSpec ns;
+  ns.mode = 4;
+  ns.fix[0] = c->nprefix;
+  ns.fix[1] = (uint32_t)(base >> 32);
+  ns.fix[2] = (uint32_t)base;
   return gcm_batch<false>(c, out, out_stride, in, in_stride, nonce_out, nonce_stride, len, nrec, nullptr, workspace,
-                          stream);
+                          stream, ns);
 }
 
 int cmpi_naive_seal_blocks(const cmpi_ctx* c, uint8_t* wire, const uint8_t* in, size_t n, size_t nblk,

@@ -125,39 +125,6 @@ __global__ __launch_bounds__(1024) void ecb_kernel(EcbArgs a) {
 namespace cmpi {
 namespace dev {
 
-// Fresh 96-bit nonces for "RAND_bytes(nonce, 12); EVP_AEAD_CTX_seal(...)" call sites
-// (alltoall.c:797, allgather.c:862, gather.c:1533, scatter.c:690, bcast.c:1537, send.c:298):
-// nonce_r = bytes 0..11 of AES_Kn(BE64(base + r) || 0^64), Kn a per-context key drawn from the
-// OS CSPRNG.  AES is a permutation, so the nonces of one context never repeat before 2^64 calls.
-struct NonceArgs {
-  uint8_t* out;
-  uint64_t stride, nrec, base;
-  const uint32_t* te0;
-  RoundKeys rk;
-};
-
-__global__ __launch_bounds__(1024) void nonce_drbg_kernel(NonceArgs a) {
-  stage_rows(a.te0, 0u);
-  __syncthreads();
-  const RowLanes rl = row_lanes(0u);
-  const RoundKeys& rk = a.rk;  // folded by the host
-  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.nrec; r += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t c = a.base + r;
-    uint32_t s0 = __builtin_bswap32((uint32_t)(c >> 32)), s1 = __builtin_bswap32((uint32_t)c), s2 = 0u, s3 = 0u;
-    aes128_enc(rk, rl, s0, s1, s2, s3);
-    u32a* o = reinterpret_cast<u32a*>(a.out + r * a.stride);
-    o[0] = s0;
-    o[1] = s1;
-    o[2] = s2;
-  }
-}
-
-}  // namespace dev
-}  // namespace cmpi
-
-namespace cmpi {
-namespace dev {
-
 // out = a ^ b over n bytes, any byte alignment (mask-ring consumption, send.c:1300-1330 /
 // recv.c:975-1002).  HBM-bound: 16 B per lane per step, grid-stride; the last n % 16 bytes
 // are done bytewise by the lanes that own them.
@@ -171,6 +138,20 @@ __global__ __launch_bounds__(256) void xor_bytes_kernel(uint8_t* out, const uint
   }
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n - 16u * nv) out[16u * nv + t] = a[16u * nv + t] ^ b[16u * nv + t];
+}
+
+// Streaming device copy (the measured HBM peak of bench.py's roofline, cmpi_debug_copy): 16 B
+// per lane, four loads in flight per lane before their stores, non-temporal both ways, a
+// grid-stride loop over the four quarters of the buffer.  nv = 16-byte units, a multiple of 4.
+__global__ __launch_bounds__(256) void copy16_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src, uint64_t nv) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, q = nv / 4u;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < q; i += stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(src + i + (uint64_t)k * q);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v[k], dst + i + (uint64_t)k * q);
+  }
 }
 
 }  // namespace dev

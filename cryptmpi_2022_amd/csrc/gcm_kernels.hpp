@@ -53,6 +53,9 @@ struct GcmArgs {
   //  3: the 12 bytes nfix[] for every record; seal also writes them at nonces + r*nonce_stride
   //     when nonces != null                                                  (600 sender, one
   //     RAND_bytes nonce per message, send.c:294-311)
+  //  4: fresh nonces, nfix[0] (4 random bytes of the context) || BE64(nfix[1]:nfix[2] + r); seal
+  //     writes them at nonces + r*nonce_stride   (RAND_bytes + seal of the naive collectives,
+  //     alltoall.c:797-801; cmpi_gcm_seal_batch_fresh)
   uint32_t nmode, nctr0, nflag, nflag2, nflag2_from;
   uint32_t nfix[3];
   // wide decomposition (gcm_flow_kernel): S steps per chunk, nch chunks per record, and the
@@ -124,10 +127,15 @@ __device__ __forceinline__ void gcm_nonce(const GcmArgs& a, uint32_t r, bool wri
     n0 = np[0];
     n1 = np[1];
     n2 = np[2];
-  } else if (a.nmode == 3u) {
+  } else if (a.nmode >= 3u) {
     n0 = a.nfix[0];
     n1 = a.nfix[1];
     n2 = a.nfix[2];
+    if (a.nmode == 4u) {  // 64-bit counter in nfix[1]:nfix[2] (host order) + r, stored big-endian
+      const uint32_t lo = n2 + r;
+      n1 = __builtin_bswap32(n1 + (lo < r ? 1u : 0u));
+      n2 = __builtin_bswap32(lo);
+    }
     if (writer && nb8) {
       u32a* np = reinterpret_cast<u32a*>(nb8);
       np[0] = n0;
@@ -216,6 +224,19 @@ __device__ __forceinline__ void build_byte_table(const u32x4* __restrict__ src, 
 // outputs of the last two steps and store a line's 8 blocks together in the step that completes
 // it, so each line reaches the L2 whole instead of as two halves a step apart; the computation's
 // schedule is unchanged.
+// Diagnostics builds only (tools/ab_build.sh ... -DCMPI_ABLATE=<bits>): parts of the lane kernel's
+// main loop switched off to measure what each costs (wrong output; never in the product build):
+// 1 progress_prio, 2 the GHASH multiply (acc ^= x), 4 the AES (keystream = counter block).
+#ifndef CMPI_ABLATE
+#define CMPI_ABLATE 0
+#endif
+// Input blocks in flight per lane in the lane kernel's main loop (loaded this many steps ahead).
+#ifndef CMPI_LANE_PREFETCH
+#define CMPI_LANE_PREFETCH 1
+#endif
+#ifndef CMPI_LANE_UNROLL
+#define CMPI_LANE_UNROLL 1
+#endif
 template <int L, bool DECRYPT, int PAIR>
 __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
   CMPI_PROBE(a, 0u);
@@ -262,7 +283,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
         cc_win = ctr >> 8;
       }
       uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = w3;
-      aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
+      if constexpr (!(CMPI_ABLATE & 4)) aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
       return u32x4{s0, s1, s2, s3};
     };
     u32x4 acc = {0u, 0u, 0u, 0u};
@@ -287,12 +308,15 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
         const int32_t nf = (int32_t)nfull;
         const uint32_t nsteps = (nfull + 3u) >> 2;
         u32x4 v = ld(q), h1 = {0u, 0u, 0u, 0u}, h2 = {0u, 0u, 0u, 0u};
+        u32x4 vn = CMPI_LANE_PREFETCH >= 2 ? ld(q + 4u) : u32x4{0u, 0u, 0u, 0u};
+        u32x4 vnn = CMPI_LANE_PREFETCH >= 3 ? ld(q + 8u) : u32x4{0u, 0u, 0u, 0u};
         auto put = [&](int32_t b, u32x4 x) {
           if (b >= 0 && b < nf) st_blk(op + 16u * (uint32_t)b, x);
         };
+#pragma unroll CMPI_LANE_UNROLL
         for (uint32_t k = 0; k < nsteps; ++k) {
           const int32_t u = 4 * (int32_t)k + (int32_t)q;
-          progress_prio(gcm_prog_off(L), ++done);
+          if constexpr (!(CMPI_ABLATE & 1)) progress_prio(gcm_prog_off(L), ++done);
           const u32x4 o = v ^ keystream(2u + x0 + (uint32_t)u);
           const int32_t j = (s0 + 4 * (int32_t)k) & 7;
           if constexpr (PAIR == 1) {
@@ -314,8 +338,21 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
           }
           h2 = h1;
           h1 = o;
-          if (u < nf) acc = gmul_byte(acc, gl, DECRYPT ? v : o);
-          v = ld((uint32_t)u + 4u);
+          if constexpr (CMPI_ABLATE & 2) {
+            if (u < nf) acc ^= DECRYPT ? v : o;
+          } else {
+            if (u < nf) acc = gmul_byte(acc, gl, DECRYPT ? v : o);
+          }
+          if constexpr (CMPI_LANE_PREFETCH >= 3) {
+            v = vn;
+            vn = vnn;
+            vnn = ld((uint32_t)u + 12u);
+          } else if constexpr (CMPI_LANE_PREFETCH == 2) {
+            v = vn;
+            vn = ld((uint32_t)u + 8u);
+          } else {
+            v = ld((uint32_t)u + 4u);
+          }
         }
         // the blocks after the last completed line
         const int32_t kl = (int32_t)nsteps - 1, jl = (s0 + 4 * kl) & 7;

@@ -41,6 +41,16 @@
  * The *_host calls use staging and scratch of their own.  Nothing is retained after a call
  * returns; device-resident work must be complete (or ordered before it) when the caller frees
  * a context or its buffers.
+ *
+ * Stream order: a device-resident call reads its inputs and writes its outputs, tags and
+ * per-record statuses in the order of `stream` ONLY.  Work the caller queued on another stream
+ * (e.g. a fill of the status array or the output buffer) is not ordered before the call unless
+ * the caller makes `stream` wait for it (an event), and results are visible to other streams
+ * only after they wait for `stream`.
+ *
+ * Errors: every call reports only failures its own HIP calls caused (a launch's own return
+ * code, never the thread's hipGetLastError state), and it neither clears nor replaces a HIP
+ * error the caller left pending in the calling thread (tests/test_gpu_errors.py).
  */
 #ifndef CMPI_AEAD_H
 #define CMPI_AEAD_H

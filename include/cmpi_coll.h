@@ -26,9 +26,12 @@
 extern "C" {
 #endif
 
-/* Seal with fresh nonces, the RAND_bytes + seal pair fused: nonce_r = bytes 0..11 of
- * AES_Kn(BE64(c + r) || 0^64), Kn drawn from the OS CSPRNG when the context was created, c a
- * per-context counter (never reused).  Nonces are written at nonce_out + r*nonce_stride. */
+/* Seal with fresh nonces, the RAND_bytes + seal pair fused into the seal kernel itself:
+ * nonce_r = P || BE64(c + r), P 4 bytes and the counter's start value 8 bytes drawn from the OS
+ * CSPRNG when the context was created, c advanced by nrec per call — the deterministic
+ * construction of SP 800-38D §8.2.1 with a random fixed field: a context never repeats a nonce,
+ * and two contexts under one key (ranks sharing CryptMPI's global key) collide only if their
+ * random fields and counter ranges both meet.  Nonces are written at nonce_out + r*nonce_stride. */
 int cmpi_gcm_seal_batch_fresh(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
                               size_t in_stride, uint8_t *nonce_out, size_t nonce_stride, size_t len, size_t nrec,
                               void *workspace, void *stream);

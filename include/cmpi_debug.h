@@ -31,11 +31,14 @@ void cmpi_debug_force_wide(int mode, uint32_t steps);
    writeback/invalidate when recorded).  event_ms: elapsed ms between two recorded events after
    the stream has been synchronised, -1 on error. */
 void* cmpi_debug_event_new(void);
+/* Streaming device-to-device copy of n bytes (n % 64 == 0, 16-byte aligned), asynchronous on
+   `stream`: bench.py's measured HBM peak (16 B per lane, 4 loads in flight, non-temporal). */
+int cmpi_debug_copy(void* dst, const void* src, size_t n, void* stream);
 int cmpi_debug_event_record(void* ev, void* stream);
 float cmpi_debug_event_ms(void* a, void* b);
 void cmpi_debug_event_free(void* ev);
-/* gcm_flow_kernel threads per workgroup: 0 automatic (512 when the batch is at most 8 waves per
- * CU, else 1024), 512 or 1024 forced (the chunk plan then assumes that many waves per CU). */
+/* gcm_flow_kernel threads per workgroup: 0 automatic (always 512 since round 4: the 1024-thread
+ * form spills), 512 or 1024 forced (the chunk plan then assumes that many waves per CU). */
 void cmpi_debug_set_flow_threads(int threads);
 /* gcm_lane_kernel (L = 4) record stores grouped by 128-byte output line (each line stored whole in
  * the step that completes it), on batches of at least one group per thread of the grid: 2 =

@@ -47,6 +47,29 @@ def test_nonces_never_repeat_across_calls():
     assert len(seen) == 256
 
 
+def test_fresh_nonce_construction():
+    """cmpi_coll.h: nonce = P || BE64(c + r) — one random field per context, a counter that
+    advances by the block count per call (both flow-kernel and lane-kernel seals), and two
+    contexts under one key draw different random fields."""
+    ctx, other = aead.AeadCtx(KEY), aead.AeadCtx(KEY)
+    ctrs = []
+    for n, p in [(1 << 20, 8), (1000, 3), (64, 70)]:
+        pt = records(0xF0 + n, p, n)
+        wire = empty(p * (n + 28), fill=0)
+        coll.seal_blocks(ctx, wire, dev(pt), n, p)
+        w = host(wire)[: p * (n + 28)].reshape(p, n + 28)
+        assert np.array_equal(w[:, 12:], oracle.gcm_seal_batch(KEY, np.ascontiguousarray(w[:, :12]), pt))
+        assert len({bytes(x[:4]) for x in w}) == 1
+        c = [int.from_bytes(bytes(x[4:12]), "big") for x in w]
+        assert c == [(c[0] + i) % (1 << 64) for i in range(p)]
+        ctrs.append((bytes(w[0, :4]), c[0], p))
+    for (pa, ca, na), (pb, cb, _) in zip(ctrs, ctrs[1:]):
+        assert pa == pb and cb == (ca + na) % (1 << 64)
+    wire = empty(28, fill=0)
+    coll.seal_blocks(other, wire, empty(1), 0, 1)
+    assert bytes(host(wire)[:4]) != ctrs[0][0]
+
+
 def test_two_rank_alltoall_in_process():
     """Rank r seals p blocks for its peers, block (r -> q) travels to rank q, q opens it."""
     p, n = 2, 4096

@@ -4,7 +4,7 @@ workload: per (round, build) a fresh process runs 3 s of back-to-back seal + ope
 power-held regime of bench.py's timed region), then times 200 steps with fence-free HIP events
 (seal and open kernel times separately) and checks the round trip.
 
-    python tools/sustained_ab.py <libA.so[@hook=v,...]> <libB.so[@hook=v,...]> [rounds] [workload]"""
+    python tools/sustained_ab.py <libA.so[@hook=v,...]> <libB.so[@hook=v,...]> [more libs] [rounds] [workload]"""
 import json
 import os
 import subprocess
@@ -50,9 +50,11 @@ def main() -> None:
     if sys.argv[1] == "--child":
         child(sys.argv[2])
         return
-    libs = sys.argv[1:3]
-    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-    workload = sys.argv[4] if len(sys.argv) > 4 else "gcm1k"
+    args = sys.argv[1:]
+    libs = [x for x in args if ".so" in x]  # two or more builds
+    rest = [x for x in args if ".so" not in x]
+    rounds = int(rest[0]) if rest else 3
+    workload = rest[1] if len(rest) > 1 else "gcm1k"
     runs = {lib: [] for lib in libs}
     for _ in range(rounds):
         for lib in libs:
