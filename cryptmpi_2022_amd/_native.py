@@ -146,6 +146,7 @@ _SIGS = {
 # only in the diagnostics build (CMPI_LIB=tools/libcmpi_aead_tools.so)
 _TOOLS_SIGS = {
     "cmpi_debug_set_wide_probe": ([_P], None),
+    "cmpi_debug_set_svc_probe": ([_P], None),
 }
 
 _lib = None
@@ -159,8 +160,12 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')"
             )
         L = ctypes.CDLL(LIB_PATH)
+        # an A/B build of an older revision (CMPI_LIB, tools/ab_build.sh) may lack newer hooks
+        lenient = bool(os.environ.get("CMPI_LIB"))
         for name, (args, res) in _SIGS.items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None) if lenient else getattr(L, name)
+            if fn is None:
+                continue
             fn.argtypes = args
             fn.restype = res
         for name, (args, res) in _TOOLS_SIGS.items():

@@ -374,6 +374,7 @@ std::atomic<int> g_flow_nt{0};          // FLOW kernel threads per workgroup: 0 
 std::atomic<int> g_flow_one_wg{1};      // FLOW kernel: one-workgroup batches finish their tags in-kernel
 #if CMPI_TOOLS
 std::atomic<uint64_t*> g_wide_probe{nullptr};  // diagnostics build: per-workgroup phase timestamps
+std::atomic<uint64_t*> g_svc_probe{nullptr};   // diagnostics build: service message phase stamps
 #endif
 // wave priority: bit 1 CTR, bit 2 OCB rotate per step (the GCM kernels: progress / rotation, fixed)
 constexpr uint32_t kSched = 7u;
@@ -1476,6 +1477,8 @@ void cmpi_debug_event_free(void* ev) {
 }
 #if CMPI_TOOLS
 void cmpi_debug_set_wide_probe(void* buf) { g_wide_probe.store(reinterpret_cast<uint64_t*>(buf)); }
+// device buffer of 8 x 32 uint64 (service_kernels.hpp SVC_STAMP); taken by the next service launch
+void cmpi_debug_set_svc_probe(void* buf) { g_svc_probe.store(reinterpret_cast<uint64_t*>(buf)); }
 #endif
 
 void cmpi_debug_force_wide(int mode, uint32_t steps) {

@@ -60,6 +60,9 @@ __device__ __forceinline__ void ctr_emit(const CtrArgs& a, uint64_t j, u32x4 ks,
 // Wave step = 64 consecutive counters in one 64-aligned counter window (lane = offset), so each
 // step's counters share bytes 0..14 and the round-1/2 cache is refilled wave-uniformly once
 // every 4 steps.  Each wave owns a contiguous run of steps; loads/stores are 1 KiB coalesced.
+#ifndef CMPI_CTR_PREFETCH
+#define CMPI_CTR_PREFETCH 1
+#endif
 template <bool XOR_IN>
 __global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
   stage_rows(a.te0, 0u);
@@ -80,7 +83,9 @@ __global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
   uint64_t win = ~0ull;
   const uint64_t nfull = a.n / 16u;
   // the next step's block is loaded right after this step's store: a whole step of AES covers it
+  // (CMPI_CTR_PREFETCH 2: two steps ahead, so a step's XOR never waits on the previous store)
   u32x4 in_cur = ctr_load<XOR_IN>(a, st0 * 64u + lane, phase, nfull);
+  u32x4 in_nxt = CMPI_CTR_PREFETCH >= 2 ? ctr_load<XOR_IN>(a, st0 * 64u + 64u + lane, phase, nfull) : u32x4{0u, 0u, 0u, 0u};
   for (uint64_t st = st0; st < st1; ++st) {
     if (a.sched & 2u) rotate_prio((uint32_t)st);
     const uint64_t v = st * 64u + lane;
@@ -94,7 +99,12 @@ __global__ __launch_bounds__(1024, 8) void ctr_kernel(CtrArgs a) {
     uint32_t s0, s1, s2, s3;
     aes128_enc_ctr(rk, rl, cc, w3, s0, s1, s2, s3);
     if (v >= phase && v - phase < a.nblk) ctr_emit<XOR_IN>(a, v - phase, u32x4{s0, s1, s2, s3}, in_cur);
-    in_cur = ctr_load<XOR_IN>(a, v + 64u, phase, nfull);
+    if constexpr (CMPI_CTR_PREFETCH >= 2) {
+      in_cur = in_nxt;
+      in_nxt = ctr_load<XOR_IN>(a, v + 128u, phase, nfull);
+    } else {
+      in_cur = ctr_load<XOR_IN>(a, v + 64u, phase, nfull);
+    }
   }
 }
 

@@ -547,7 +547,9 @@ __device__ __forceinline__ u32x4 flow_tree_r4(u32x4 acc, uint32_t lane) {
 // record and round, the record's last arriving workgroup XORs that record's partials, per-stream
 // zeroed counters — was also slower: 8 x 1 MiB 23.5 vs 21.1 us, 1 x 64 KiB 14.6 vs 13.4, 1 x 8 MiB
 // 24.5 vs 21.9 (profiles/r03f_flow_fused_ab.txt): store drain + add round trip + partial loads on
-// the last workgroup's path cost more than the launch boundary.)
+// the last workgroup's path cost more than the launch boundary.  Round 5 re-measured a one-counter
+// form (grid's last arriver finishes every record, counter zeroed by hipStreamWriteValue32): 29.8
+// vs 19.3 us, of which the stream write alone costs 7.7 us per call (profiles/r05j_*, r05k_*).)
 // Unit u = (record r, chunk i) of a flow decomposition: chunk 0 absorbs the remainder (r0 X-blocks,
 // ceil(r0/64) steps), the others are C = 64·S X-blocks; returns the base X position of lane 0's
 // first step.

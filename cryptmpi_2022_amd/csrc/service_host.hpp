@@ -171,6 +171,9 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
   a.life_ticks = kSvcLifeUs * 100u;
   a.cap_ticks = (kSvcLifeUs + 100000u) * 100u;
   a.rk = folded(c->rk);
+#if CMPI_TOOLS
+  a.probe = g_svc_probe.load();
+#endif
   HIP_TRY(hipMemsetAsync(S.go + 16, 0, 4, S.st));  // arrival counter
   void* kargs[] = {&a};
   HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(cmpi::dev::gcm_service_kernel), dim3(cmpi::dev::kSvcGroups),

@@ -71,8 +71,27 @@ struct SvcArgs {
   uint32_t ls_min;       // smallest chunk-step exponent (test hook cmpi_debug_set_svc_ls_min; 0)
   uint32_t gen;
   uint64_t idle_ticks, life_ticks, cap_ticks;  // 100 MHz wall clock
+#if CMPI_TOOLS
+  uint64_t* probe;  // diagnostics build: per-message phase stamps (cmpi_debug_set_svc_probe), or null
+#endif
   RoundKeys rk;
 };
+
+// Diagnostics build only (-DCMPI_TOOLS=1, tools/svc_timeline.py): 100 MHz wall-clock stamps of a
+// message's phases into probe[32 * (seq % 8) + slot]: 0 the leader sees the seq in the host ring,
+// 1 the descriptor is in the leader workgroup's LDS (and published), 2 + wg a workgroup starts
+// the message, 10 + wg its waves' record stores are performed, 18 + wg its partial is published
+// and counted, 26 the last arriver has the tag / verdict, 27 the completion words are issued.
+#if CMPI_TOOLS
+#define SVC_STAMP(s, seq, slot)                                                                       \
+  do {                                                                                                \
+    if ((s).probe) (s).probe[32u * ((seq) & 7u) + (slot)] = wall_clock64();                           \
+  } while (0)
+#else
+#define SVC_STAMP(s, seq, slot) \
+  do {                          \
+  } while (0)
+#endif
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -159,6 +178,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   const uint64_t cbits = (uint64_t)len * 8u;
   const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
   const uint32_t u = wg * wpb + wv;
+  if (threadIdx.x == 0u) SVC_STAMP(s, seq, 2u + wg);
   u32x4 pw = {0u, 0u, 0u, 0u};
   if (u < nch) {
     uint32_t r;
@@ -168,6 +188,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores are performed
   __syncthreads();
   if (threadIdx.x == 0u) {
+    SVC_STAMP(s, seq, 10u + wg);
     u32x4 x = lds128(kFlowAgg);
     for (uint32_t j = 1; j < wpb; ++j) x ^= lds128(kFlowAgg + 16u * j);
     uint32_t last = 1u;
@@ -182,6 +203,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
     }
     lds_st32(kSvcX + 56u, last);
     lds_st128(kSvcTag, x);
+    SVC_STAMP(s, seq, 18u + wg);
   }
   __syncthreads();
   if (!lds32(kSvcX + 56u)) return;  // workgroup-uniform
@@ -193,6 +215,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
       ok = (d[0] | d[1] | d[2] | d[3]) == 0u ? 1u : 0u;
     }
     lds_st32(kSvcX + 60u, ok);
+    SVC_STAMP(s, seq, 26u);
   }
   __syncthreads();
   if (DECRYPT && !lds32(kSvcX + 60u)) {  // forged: zero-fill the plaintext (after every workgroup's stores)
@@ -209,6 +232,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
     sys_store16(s.done, u32x4{seq, lds32(kSvcX + 60u), seq, tag[0]});
     sys_store16(s.done + 4, u32x4{seq, tag[1], seq, tag[2]});
     sys_store16(s.done + 8, u32x4{seq, tag[3], 0u, 0u});
+    SVC_STAMP(s, seq, 27u);
   }
 }
 
@@ -315,6 +339,7 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
             d[6] = c2[1], d[7] = c2[2], d[8] = c2[3];
             d[9] = c3[1], d[10] = c3[2], d[11] = c3[3];
             if (d[0] == kSvcStop) ex = 1u;
+            SVC_STAMP(s, q, 0u);
             break;
           }
           const uint64_t now = wall_clock64();
@@ -368,6 +393,7 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
           __builtin_amdgcn_s_sleep(4);
         }
       }
+      if (leader && !ex) SVC_STAMP(s, q, 1u);
       lds_st32(kSvcX, ex);
       lds_st32(kSvcX + 4u, q);
 #pragma unroll

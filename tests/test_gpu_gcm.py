@@ -272,6 +272,25 @@ def test_flow_kernel_forms(threads, n, nrec, steps):
     assert list(st) == [1] * nrec and np.array_equal(back, pt)
 
 
+def test_flow_open_without_status():
+    """Config 5's shape (8 x 1 MiB, the default plan: 256 workgroups + the XOR combine) opened
+    with status == NULL and one forged record: the record is zero-filled, the others are intact,
+    and seals right after on the same stream are bit-exact."""
+    n, nrec = 1 << 20, 8
+    ctx = aead.AeadCtx(KEY)
+    pt = records(0x7E00, nrec, n)
+    nonces = random_nonces(0x7E01, nrec)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    forged = want.copy()
+    forged[5, 12345] ^= 0x04
+    out = empty(nrec * n, fill=0xAA)
+    ctx.open_batch(out, dev(forged), dev(nonces), n, nrec)
+    b = host(out)[: nrec * n].reshape(nrec, n)
+    assert not b[5].any() and np.array_equal(b[[0, 1, 2, 3, 4, 6, 7]], pt[[0, 1, 2, 3, 4, 6, 7]])
+    for _ in range(3):
+        assert np.array_equal(gpu_seal(ctx, nonces, pt), want)
+
+
 def test_flow_two_streams_one_fresh_context():
     """calls on one context from two streams at once — the first use of a chunk-weight
     table by either — stay correct: seals of 8 x 1 MiB and

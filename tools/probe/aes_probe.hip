@@ -40,6 +40,31 @@ __device__ __forceinline__ void enc_round4(uint32_t la, uint32_t lb, uint32_t m,
   s3 = xor3(d0, d1, xor3(d2, d3, k3));
 }
 
+// SDWA lookup address: the lane constant lc (bytes 0, 2, 3) stays in A; byte 1 <- byte R of s
+template <int R>
+__device__ __forceinline__ uint32_t sdwa_addr(uint32_t& A, uint32_t s) {
+  if constexpr (R == 0) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(A) : "v"(s));
+  if constexpr (R == 1) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(A) : "v"(s));
+  if constexpr (R == 2) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(A) : "v"(s));
+  if constexpr (R == 3) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(A) : "v"(s));
+  return A;
+}
+struct SdwaRegs {
+  uint32_t a[16];
+};
+__device__ __forceinline__ void enc_round_sdwa(SdwaRegs& A, uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                               uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  // A.a[4c + r]: lane constant of the lookup of row r of column c (Te0 half for r even, Te1 odd)
+  const uint32_t a0 = lds32(sdwa_addr<0>(A.a[0], s0)), a1 = lds32(sdwa_addr<1>(A.a[1], s1)), a2 = lds32(sdwa_addr<2>(A.a[2], s2)), a3 = lds32(sdwa_addr<3>(A.a[3], s3));
+  const uint32_t b0 = lds32(sdwa_addr<0>(A.a[4], s1)), b1 = lds32(sdwa_addr<1>(A.a[5], s2)), b2 = lds32(sdwa_addr<2>(A.a[6], s3)), b3 = lds32(sdwa_addr<3>(A.a[7], s0));
+  const uint32_t c0 = lds32(sdwa_addr<0>(A.a[8], s2)), c1 = lds32(sdwa_addr<1>(A.a[9], s3)), c2 = lds32(sdwa_addr<2>(A.a[10], s0)), c3 = lds32(sdwa_addr<3>(A.a[11], s1));
+  const uint32_t d0 = lds32(sdwa_addr<0>(A.a[12], s3)), d1 = lds32(sdwa_addr<1>(A.a[13], s0)), d2 = lds32(sdwa_addr<2>(A.a[14], s1)), d3 = lds32(sdwa_addr<3>(A.a[15], s2));
+  s0 = xor3(a0, a1, rotl16(xor3(a2, a3, k0)));
+  s1 = xor3(b0, b1, rotl16(xor3(b2, b3, k1)));
+  s2 = xor3(c0, c1, rotl16(xor3(c2, c3, k2)));
+  s3 = xor3(d0, d1, rotl16(xor3(d2, d3, k3)));
+}
+
 template <int VAR>
 __global__ void probe(const uint32_t* te0, RoundKeys k, uint32_t* out, unsigned long long* cyc) {
   stage_rows(te0, 65536u);
@@ -53,6 +78,12 @@ __global__ void probe(const uint32_t* te0, RoundKeys k, uint32_t* out, unsigned 
   __syncthreads();
   const RowLanes L = row_lanes(65536u);
   const uint32_t lbB = (threadIdx.x & 31u) << 2;
+  SdwaRegs SA;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    SA.a[i] = (i & 1) ? L.l1 : L.l0;
+    asm volatile("" : "+v"(SA.a[i]));
+  }
   uint32_t s0 = threadIdx.x * 0x9e3779b9u, s1 = blockIdx.x, s2 = s0 ^ 0x1234567u, s3 = ~s0;
   uint32_t t0 = s0 ^ 1u, t1 = s1 ^ 2u, t2 = s2 ^ 3u, t3 = s3 ^ 4u;
   const uint64_t c0 = __builtin_amdgcn_s_memtime();
@@ -67,6 +98,14 @@ __global__ void probe(const uint32_t* te0, RoundKeys k, uint32_t* out, unsigned 
       s3 ^= k.w[3];
 #pragma unroll
       for (int r = 1; r < 10; ++r) enc_round4(L.l0, lbB, L.m, s0, s1, s2, s3, k.w[4 * r], k.w[4 * r + 1], k.w[4 * r + 2], k.w[4 * r + 3]);
+      enc_last(L, s0, s1, s2, s3, k.w[40], k.w[41], k.w[42], k.w[43]);
+    } else if constexpr (VAR == 3) {
+      s0 ^= k.w[0];
+      s1 ^= k.w[1];
+      s2 ^= k.w[2];
+      s3 ^= k.w[3];
+#pragma unroll
+      for (int r = 1; r < 10; ++r) enc_round_sdwa(SA, s0, s1, s2, s3, k.w[4 * r], k.w[4 * r + 1], k.w[4 * r + 2], k.w[4 * r + 3]);
       enc_last(L, s0, s1, s2, s3, k.w[40], k.w[41], k.w[42], k.w[43]);
     } else {
       if (b & 1) continue;
@@ -137,5 +176,7 @@ int main() {
   run<0>("rows_te01_rotl16", 8, te0, k, out, cyc, ncu);
   run<2>("rows_te01_rotl16_two_blocks", 4, te0, k, out, cyc, ncu);
   run<1>("rows_te0123_norot", 4, te0, k, out, cyc, ncu);
+  run<3>("rows_te01_sdwa_addr", 4, te0, k, out, cyc, ncu);
+  run<3>("rows_te01_sdwa_addr", 8, te0, k, out, cyc, ncu);
   return 0;
 }

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define CK(x)                                                                       \
   do {                                                                              \
@@ -63,7 +64,16 @@ __global__ void probe(uint32_t* out, uint32_t seed, unsigned long long* cyc) {
       if constexpr (OP == 13) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
       if constexpr (OP == 14) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(x));
       if constexpr (OP == 15) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x) : "s"(sk));
-      if constexpr (OP >= 20) {
+      if constexpr (OP == 30) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(x) : "v"(y));
+      if constexpr (OP == 31) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(x) : "v"(y));
+      if constexpr (OP == 32) asm volatile("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "=v"(x) : "v"(y), "v"(z));
+      if constexpr (OP == 33) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+      if constexpr (OP == 34) asm volatile("v_and_b32 %0, 0xff00, %0" : "+v"(x));
+      if constexpr (OP == 35) asm volatile("v_alignbyte_b32 %0, %0, %1, 2" : "+v"(x) : "v"(y));
+      if constexpr (OP == 36) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "+v"(x) : "v"(y));
+      if constexpr (OP == 37) asm volatile("v_lshlrev_b32 %0, %1, %0" : "+v"(x) : "v"(y));
+      if constexpr (OP == 39) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z));
+      if constexpr (OP >= 20 && OP < 30) {
         if constexpr (OP == 20 || OP == 21 || OP == 22) {
           const uint32_t a = ((x & 0xff00u) | lb);
           uint32_t t;
@@ -133,6 +143,18 @@ int main() {
   unsigned long long* cyc;
   CK(hipMalloc(&out, 4u * ncu * 2048));
   CK(hipMalloc(&cyc, 16u * ncu * 32));
+  for (int wps : {4}) {
+    run<30>("v_mov_b32_sdwa_byte1_preserve_from_byte0", wps, 1, 0, out, cyc, ncu);
+    run<31>("v_mov_b32_sdwa_byte1_preserve_from_byte2", wps, 1, 0, out, cyc, ncu);
+    run<32>("v_or_b32_sdwa_src0_byte2", wps, 1, 0, out, cyc, ncu);
+    run<33>("v_bfi_b32_vvv", wps, 1, 0, out, cyc, ncu);
+    run<34>("v_and_b32_literal", wps, 1, 0, out, cyc, ncu);
+    run<35>("v_alignbyte_b32", wps, 1, 0, out, cyc, ncu);
+    run<36>("v_xor_b32_sdwa_word1", wps, 1, 0, out, cyc, ncu);
+    run<37>("v_lshlrev_b32_vgpr", wps, 1, 0, out, cyc, ncu);
+    run<39>("v_add3_u32", wps, 1, 0, out, cyc, ncu);
+  }
+  if (getenv("PROBE_SDWA_ONLY")) return 0;
   for (int wps : {2, 4}) {
     run<0>("v_xor_b32", wps, 1, 0, out, cyc, ncu);
     run<1>("v_and_b32", wps, 1, 0, out, cyc, ncu);
