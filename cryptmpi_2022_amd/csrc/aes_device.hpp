@@ -291,10 +291,15 @@ __device__ __forceinline__ void stage_copy(const u32x4* __restrict__ src, uint32
 
 // ---------------------------------------------------------------- GHASH
 // Lane constants for the conflict-free byte-table multiply.
+#ifndef CMPI_GHASH_B1
+#define CMPI_GHASH_B1 0
+#endif
 struct GhashLane {
   uint32_t sh;        // 8 * (k & 3), k = lane & 15
   bool q1, q2;        // bits of k >> 2
   uint32_t po[4];     // po[j].byte[i] = ((4j + i + k) & 15) * 16
+  uint32_t p1[4];     // CMPI_GHASH_B1: ((4j + 1 + k) & 15) * 16 in byte 0 (byte-1 positions by bitop3)
+  uint32_t m;         // 0xff00 in a VGPR
 };
 __device__ __forceinline__ GhashLane ghash_lane() {
   GhashLane g;
@@ -308,7 +313,9 @@ __device__ __forceinline__ GhashLane ghash_lane() {
 #pragma unroll
     for (int i = 0; i < 4; ++i) w |= (((4u * j + i + k) & 15u) << 4) << (8 * i);
     g.po[j] = w;
+    g.p1[j] = ((4u * j + 1u + k) & 15u) << 4;
   }
+  g.m = byte1_mask();
   return g;
 }
 
@@ -339,12 +346,17 @@ __device__ __forceinline__ u32x4 gmul_byte(u32x4 x, const GhashLane& g, u32x4 y 
     }
     return r;
   }
+  auto gaddr = [&](int p) -> uint32_t {
+    if constexpr (CMPI_GHASH_B1 != 0) {
+      if ((p & 3) == 1) return __builtin_amdgcn_bitop3_b32(w[p >> 2], g.m, g.p1[p >> 2], 0xEA);  // (w & 0xff00) | p1
+    }
+    const uint32_t sel = 0x0c0c0000u | ((4u + (p & 3)) << 8) | (uint32_t)(p & 3);
+    return perm(w[p >> 2], g.po[p >> 2], sel);
+  };
 #pragma unroll
   for (int t = 0; t < 16; t += 2) {
-    const uint32_t sa = 0x0c0c0000u | ((4u + (t & 3)) << 8) | (uint32_t)(t & 3);
-    const uint32_t sb = 0x0c0c0000u | ((4u + ((t + 1) & 3)) << 8) | (uint32_t)((t + 1) & 3);
-    const u32x4 e1 = lds128(perm(w[t >> 2], g.po[t >> 2], sa));
-    const u32x4 e2 = lds128(perm(w[(t + 1) >> 2], g.po[(t + 1) >> 2], sb));
+    const u32x4 e1 = lds128(gaddr(t));
+    const u32x4 e2 = lds128(gaddr(t + 1));
 #pragma unroll
     for (int c = 0; c < 4; ++c) r[c] = xor3(r[c], e1[c], e2[c]);
   }

@@ -71,6 +71,7 @@ struct GcmArgs {
   uint32_t one_wg;
 #if CMPI_TOOLS
   uint64_t* probe;  // per-WG phase timestamps (cmpi_debug_set_wide_probe), or null
+  uint64_t* unit_stamps;  // service messages: wave 0 of workgroup 0's unit phases (slots 28..31)
 #endif
   RoundKeys rk;
 };
@@ -237,6 +238,10 @@ __device__ __forceinline__ void build_byte_table(const u32x4* __restrict__ src, 
 #ifndef CMPI_LANE_UNROLL
 #define CMPI_LANE_UNROLL 1
 #endif
+// progress_prio every CMPI_PRIO_EVERY steps of the line-store loop
+#ifndef CMPI_PRIO_EVERY
+#define CMPI_PRIO_EVERY 1
+#endif
 template <int L, bool DECRYPT, int PAIR>
 __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
   CMPI_PROBE(a, 0u);
@@ -316,7 +321,9 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
 #pragma unroll CMPI_LANE_UNROLL
         for (uint32_t k = 0; k < nsteps; ++k) {
           const int32_t u = 4 * (int32_t)k + (int32_t)q;
-          if constexpr (!(CMPI_ABLATE & 1)) progress_prio(gcm_prog_off(L), ++done);
+          if constexpr (!(CMPI_ABLATE & 1)) {
+            if (CMPI_PRIO_EVERY == 1 || k % CMPI_PRIO_EVERY == 0u) progress_prio(gcm_prog_off(L), ++done);
+          }
           const u32x4 o = v ^ keystream(2u + x0 + (uint32_t)u);
           const int32_t j = (s0 + 4 * (int32_t)k) & 7;
           if constexpr (PAIR == 1) {
@@ -630,6 +637,13 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
     va = prefetch(0);
     vb = prefetch(1);
   }
+#if CMPI_TOOLS
+  auto ustamp = [&](uint32_t slot) {
+    if (a.unit_stamps && blockIdx.x == 0u && threadIdx.x == 0u) a.unit_stamps[slot] = wall_clock64();
+  };
+#else
+  auto ustamp = [](uint32_t) {};
+#endif
   uint32_t it = 0;
   // E_K(J0), folded into chunk 0's partial (only lane 0's copy is used).  Chunk 0 holds the
   // r0 = G..2G-1 leading positions, so its first step is partial whenever 64 does not divide
@@ -641,13 +655,16 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
     rotate_prio(it++);
     const u32x4 ks = keystream(k == 0u && j0_step0 && lane == 0u ? 1u : ctr_of(k));
     if (k == 0u) ekj = ks;
+    if (k == 0u) ustamp(28u);  // first keystream done (cache fill + one AES pass)
     consume_ks(k, va, ks);
+    if (k == 0u) ustamp(29u);  // its input block arrived, ct stored, Horner step
     va = prefetch(k + 2u);
     if (k + 1u < steps) consume_ks(k + 1u, vb, keystream(ctr_of(k + 1u)));
     vb = prefetch(k + 3u);
   }
   if (!j0_step0) ekj = i == 0u ? keystream(1u) : u32x4{0u, 0u, 0u, 0u};
   if (pre) CMPI_PROBE(a, 2u);
+  ustamp(30u);  // all steps done
   u32x4 V = flow_tree_r4(acc, lane);
 #pragma unroll
   for (int c = 0; c < 4; ++c) V[c] = (uint32_t)__builtin_amdgcn_readfirstlane(V[c]);
@@ -659,6 +676,7 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
     if (i == 0u && lane == 0u) a.ekj0[r] = ekj;
   }
   if (pre) CMPI_PROBE(a, 5u);
+  ustamp(31u);  // lane tree + chunk weight done
   return pw;
 }
 

@@ -45,7 +45,7 @@ struct Svc {
   bool launched = false;
   uint32_t* hw = nullptr;      // page-locked coherent: ring [0..15] (four 16-B chunks), kick [16], done [32..44]
   uint32_t* dw = nullptr;      // its device address
-  uint32_t* go = nullptr;      // device control words (64 B), counter (at +64), partials (at +128)
+  uint32_t* go = nullptr;      // device control area: counter (at +64), partials (at +128), published units (at +256)
   cmpi::dev::u32x4* wts = nullptr;  // device chunk weights (4 x 64 x 4 blocks)
   bool wts_ok = false;
   uint8_t* bounce = nullptr;   // page-locked: pageable messages
@@ -81,7 +81,7 @@ constexpr size_t kSvcWtsBytes = 4 * 64 * 4 * 16;
 // H), the workgroup partials, the bounce buffer's last message.  Stream drained.
 void svc_wipe(Svc& S) {
   wipe_dev(S.wts, kSvcWtsBytes);
-  wipe_dev(S.go, 256);
+  wipe_dev(S.go, cmpi::dev::kSvcGoBytes);
   if (S.bounce) memset(S.bounce, 0, S.bcap);
   S.wts_ok = false;
   wipe_sync();  // svc_weights' next upload must land after the wipe
@@ -384,8 +384,8 @@ int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
   S.slot = (int)(g_svc_next_slot[c->device].fetch_add(1) % kSvcSlots);
   if (hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&S.hw, 256, hipHostMallocCoherent) != hipSuccess ||
-      hipHostGetDevicePointer((void**)&S.dw, S.hw, 0) != hipSuccess || hipMalloc((void**)&S.go, 256) != hipSuccess ||
-      hipMalloc((void**)&S.wts, kSvcWtsBytes) != hipSuccess || hipMemset(S.go, 0, 256) != hipSuccess) {
+      hipHostGetDevicePointer((void**)&S.dw, S.hw, 0) != hipSuccess || hipMalloc((void**)&S.go, cmpi::dev::kSvcGoBytes) != hipSuccess ||
+      hipMalloc((void**)&S.wts, kSvcWtsBytes) != hipSuccess || hipMemset(S.go, 0, cmpi::dev::kSvcGoBytes) != hipSuccess) {
     svc_release(S);
     delete c->svc;
     c->svc = nullptr;

@@ -11,15 +11,18 @@
 //   leader (workgroup 0, one lane): polls the three chunks with one 16-byte system-scope load each
 //           (a 16-byte read is one snapshot of its chunk, so a chunk showing the new seq shows its
 //           new words: the descriptor arrives with the seq, no second round trip); on a new seq in
-//           all three it copies the
-//           descriptor to device memory (go[4..12], write-through) and publishes go[1] = seq,
-//           both under a seqlock (go[3] odd while they change: a workgroup that sat out the last
-//           message may be reading them);
+//           all three it publishes the descriptor for the other workgroups as 13 self-tagged
+//           8-byte units {seq, word} (the 12 descriptor words and the generation) in device memory
+//           (agent-scope stores, none waited: a unit is one snapshot, so no seqlock — round 5: the
+//           seqlock's three drains and the readers' two-phase reads took 1.7 + 1.5 us of each
+//           64 KiB message, tools/svc_timeline.py);
 //           on idle / lifetime / op STOP / a kick (the host word kick == gen: another context's
-//           service takes this stream slot) it publishes go[2] = 1, writes done[12] = gen and exits.
-//           A message whose chunks fit one workgroup is served by the leader's workgroup alone
-//           and not published (the others act only on a change of go[1]).
-//   others: poll go[] (write-through loads), run their share, exit on go[2].
+//           service takes this stream slot) it publishes a STOP descriptor, writes done[12] = gen
+//           and exits.  A message whose chunks fit one workgroup is served by the leader's
+//           workgroup alone and not published.
+//   others: poll the 13 units (agent-scope loads, all in flight together) until every unit
+//           carries one seq != the last one seen and the generation unit names theirs; run their
+//           share, exit on STOP.
 //   message: the flow decomposition (gcm_flow_kernel's unit code): chunks of C = 64·S X-blocks,
 //           S the smallest power of two <= 8 with at most 64 chunks, one wavefront per chunk,
 //           8 chunks per workgroup; every chunk's partial is weighted by H^(1 + (nch-1-i)C) (host
@@ -55,13 +58,15 @@ constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u, kSvcXor = 3u, kS
 // mask lo/hi at 6..7, CTR counter block as big-endian halves hi lo/hi, lo lo/hi at 8..11
 constexpr uint32_t kSvcDesc = 12u;
 constexpr uint32_t kSvcChunks = kSvcDesc / 3u;  // ring chunks {seq, three descriptor words}
+constexpr uint32_t kSvcPubWords = 64u;          // go[64 + 2u .. 2u + 1]: published unit u = {seq, word}
+constexpr uint32_t kSvcGoBytes = 512u;          // the device control area (host: hipMalloc)
 constexpr uint32_t kSvcMaxStreamLen = 65536u;   // counter-mode ops: the 702 ring's small messages
 
 struct SvcArgs {
   const uint32_t* ring;  // page-locked host words (device address): chunks [4c] = seq, [4c+1..4c+3] = desc[3c..3c+2]
   const uint32_t* kick;  // page-locked host word: == gen asks this generation to exit (its stream slot is wanted)
   uint32_t* done;        // page-locked host words: [0..9] five {seq, word} pairs (status, tag 0-3), [12] exited generation
-  uint32_t* go;          // device: [0] generation, [1] seq, [2] exit, [3] seqlock version, [4..15] descriptor copy
+  uint32_t* go;          // device: [16] arrival counter, [32..63] partials, [64..89] 13 published units {seq, word}
   uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
   u32x4* part;           // device: one partial per workgroup
   const u32x4* wts;      // device: 4 x 64 x 4; wts[256s + 4k + 3] = H^(1 + (63-k)·64·2^s)
@@ -81,7 +86,8 @@ struct SvcArgs {
 // message's phases into probe[32 * (seq % 8) + slot]: 0 the leader sees the seq in the host ring,
 // 1 the descriptor is in the leader workgroup's LDS (and published), 2 + wg a workgroup starts
 // the message, 10 + wg its waves' record stores are performed, 18 + wg its partial is published
-// and counted, 26 the last arriver has the tag / verdict, 27 the completion words are issued.
+// and counted, 26 the last arriver has the tag / verdict, 27 the completion words are issued;
+// 28..31 workgroup 0's first unit: first keystream, first step consumed, steps done, tree + weight.
 #if CMPI_TOOLS
 #define SVC_STAMP(s, seq, slot)                                                                       \
   do {                                                                                                \
@@ -123,6 +129,33 @@ __device__ __forceinline__ u32x4 wt_load16(const u32x4* p) {
   const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// The leader's descriptor for the other workgroups: units 0..11 = {seq, d[j]}, unit 12 = {seq, gen}.
+__device__ __forceinline__ void svc_publish(uint32_t* go, uint32_t seq, uint32_t gen, const uint32_t (&d)[kSvcDesc]) {
+  uint64_t* u = reinterpret_cast<uint64_t*>(go + kSvcPubWords);
+#pragma unroll
+  for (uint32_t j = 0; j < kSvcDesc; ++j)
+    __hip_atomic_store(u + j, (uint64_t)seq | ((uint64_t)d[j] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(u + kSvcDesc, (uint64_t)seq | ((uint64_t)gen << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// A reader's poll: true with (seq, d) when all 13 units carry one seq != cur and the generation
+// unit names `gen`.
+__device__ __forceinline__ bool svc_take(const uint32_t* go, uint32_t cur, uint32_t gen, uint32_t& seq,
+                                         uint32_t (&d)[kSvcDesc]) {
+  const uint64_t* u = reinterpret_cast<const uint64_t*>(go + kSvcPubWords);
+  uint64_t v[kSvcDesc + 1];
+#pragma unroll
+  for (uint32_t j = 0; j <= kSvcDesc; ++j) v[j] = __hip_atomic_load(u + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t q = (uint32_t)v[kSvcDesc];
+  if (q == cur || (uint32_t)(v[kSvcDesc] >> 32) != gen) return false;
+#pragma unroll
+  for (uint32_t j = 0; j < kSvcDesc; ++j) {
+    if ((uint32_t)v[j] != q) return false;
+    d[j] = (uint32_t)(v[j] >> 32);
+  }
+  seq = q;
+  return true;
 }
 
 // LDS words shared by the workgroup (inside the flow aggregation area)
@@ -174,6 +207,9 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   a.nch = nch;
   a.r0 = nx - (nch - 1u) * C;
   a.chw = s.wts + 256u * ls + 4u * (kSvcMaxChunks - nch);  // a.chw[4i + 3] = H^(1 + (nch-1-i)C)
+#if CMPI_TOOLS
+  a.unit_stamps = s.probe ? s.probe + 32u * (seq & 7u) : nullptr;
+#endif
   if (wg >= ngrp) return;
   const uint64_t cbits = (uint64_t)len * 8u;
   const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
@@ -194,7 +230,11 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
     uint32_t last = 1u;
     if (ngrp > 1u) {
       wt_store16(s.part + wg, x);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this XCD's L2 (the record bytes) back to the host
+      // whole record blocks are write-through stores the waves drained above (and the partial an
+      // agent-scope store): no L2 write-back before the add — only a message with a partial last
+      // block has plain byte stores to release (round 5: the fence was 1.7 us of each arrival)
+      if (len & 15u) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       last = __hip_atomic_fetch_add(s.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngrp - 1u ? 1u : 0u;
       if (last) {
         x = wt_load16(s.part);
@@ -313,14 +353,6 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
   const uint64_t t0 = wall_clock64();
   uint64_t t_last = t0;
   uint32_t cur = s.seq0;
-  uint32_t ver = 0u;  // leader: the descriptor seqlock's version (go[3], even when stable)
-  if (leader && threadIdx.x == 0u) {  // this generation's control words
-    ver = wt_load(s.go + 3) & ~1u;
-    wt_store(s.go + 1, cur);
-    wt_store(s.go + 2, 0u);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    wt_store(s.go, s.gen);
-  }
   for (;;) {
     if (threadIdx.x == 0u) {
       uint32_t ex = 0u, q = cur;
@@ -352,45 +384,25 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
           __builtin_amdgcn_s_sleep(2);
         }
         uint32_t ls_, nch_;
-        if (!ex && d[0] <= kSvcOpen && svc_plan(d[1], ls_, nch_, s.ls_min) > 1u) {  // seqlock: version odd while the descriptor is rewritten
-          wt_store(s.go + 3, ++ver);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-          for (uint32_t j = 0; j < kSvcDesc; ++j) wt_store(s.go + 4u + j, d[j]);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          wt_store(s.go + 1, q);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          wt_store(s.go + 3, ++ver);
-        } else if (ex) {
-          wt_store(s.go + 2, 1u);
+        if (!ex && d[0] <= kSvcOpen && svc_plan(d[1], ls_, nch_, s.ls_min) > 1u) {
+          svc_publish(s.go, q, s.gen, d);
+        } else if (ex) {  // a STOP descriptor under a seq no message uses
+          uint32_t st[kSvcDesc] = {};
+          st[0] = kSvcStop;
+          svc_publish(s.go, cur ^ 0x80000000u, s.gen, st);
         }  // a message of one workgroup's chunks is the leader's alone: nothing to publish
       } else {
         for (;;) {
-          if (wt_load(s.go) == s.gen) {
-            if (wt_load(s.go + 2)) {
-              ex = 1u;
-              break;
-            }
-            // a workgroup that sat out the last message may look while the leader rewrites the
-            // descriptor for the next one: take (seq, descriptor) only from one stable version
-            const uint32_t v1 = wt_load(s.go + 3);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (!(v1 & 1u)) {
-              q = wt_load(s.go + 1);
-#pragma unroll
-              for (uint32_t j = 0; j < kSvcDesc; ++j) d[j] = wt_load(s.go + 4u + j);
-              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-              const uint32_t v2 = wt_load(s.go + 3);
-              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-              if (v2 == v1 && q != cur) break;
-              q = cur;
-            }
+          if (svc_take(s.go, cur, s.gen, q, d)) {
+            if (d[0] == kSvcStop) ex = 1u;
+            break;
           }
+          q = cur;
           if (wall_clock64() - t0 > s.cap_ticks) {  // bound: the leader exits long before this
             ex = 1u;
             break;
           }
-          __builtin_amdgcn_s_sleep(4);
+          __builtin_amdgcn_s_sleep(2);
         }
       }
       if (leader && !ex) SVC_STAMP(s, q, 1u);

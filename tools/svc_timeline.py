@@ -82,6 +82,9 @@ def main():
                     "arrive": med(arr - np.where(act, r[:, 10:18], -np.inf).max(axis=1)),
                     "finish": med(r[:, 26] - arr), "complete": med(r[:, 27] - r[:, 26]),
                     "gpu_span": med(r[:, 27]), "host_call": med(host),
+                    # workgroup 0's first unit (chunk 0 on the single-workgroup shapes), from its start
+                    "u_first_keystream": med(r[:, 28] - r[:, 2]), "u_first_step": med(r[:, 29] - r[:, 2]),
+                    "u_steps_done": med(r[:, 30] - r[:, 2]), "u_tree_weight": med(r[:, 31] - r[:, 2]),
                 }
                 print(json.dumps({f"{op}_{n}": res[f"{op}_{n}"]}), flush=True)
     finally:
