@@ -1359,6 +1359,7 @@ def main() -> None:
         ok = ok and ok_p
         if args.pipelined:
             wall = wall_pipe
+    pipelined = args.pipelined and wall_pipe is not None
     parity = w.parity_cpu() if rank == 0 else None  # outside the timed region
     per_rank_bytes = w.n * w.nrec  # plaintext bytes per step per rank
     wall_max, value = aggregate(wall, per_rank_bytes, args.steps, pg, w.dev)
@@ -1378,7 +1379,7 @@ def main() -> None:
         "ms_per_step": round(wall_max / args.steps * 1e3, 4),
         "ms_per_step_serial": round(wall_serial / args.steps * 1e3, 4),
         "ms_per_step_pipelined": None if wall_pipe is None else round(wall_pipe / args.steps * 1e3, 4),
-        "headline_schedule": "pipelined (two streams)" if (args.pipelined and wall_pipe is not None) else "serial (one stream)",
+        "headline_schedule": "pipelined (two streams)" if pipelined else "serial (one stream)",
         "steps_timed_as": ("two streams: the seal of batch i+1 overlaps the open of batch i (double-buffered); "
                            "every step seals and opens the whole batch") if pipelined else "one stream, seal then open",
         "higher_is_better": True,

@@ -476,8 +476,10 @@ __device__ __forceinline__ uint32_t flow_tab(uint32_t f) {  // nibble table f (k
 // building the nibble tables in LDS from their ten multipliers with nib_row_to_lds — 160 B fetched
 // instead of 80 KiB — staged at 5.4 us instead of 2.6 on 8 x 1 MiB: the 320 rows' VALU + 80 KiB
 // of ds_write_b128 cost more than the L2 round trip.)
+// (stage_flow_tables: the loads and stores only, by threads 0..NT-1 — the resident service runs
+// more threads than it stages with; stage_flow adds the workgroup barrier.)
 template <int NT>
-__device__ __forceinline__ void stage_flow(const GcmArgs& a) {
+__device__ __forceinline__ void stage_flow_tables(const GcmArgs& a) {
   constexpr int kR = 1024 / NT, kW = 5120 / NT;  // loads per thread
   uint32_t rv[kR];
   u32x4 wv[kW];
@@ -502,6 +504,10 @@ __device__ __forceinline__ void stage_flow(const GcmArgs& a) {
     const uint32_t e = t + j * NT;
     lds_st128(flow_tab(e >> 9) + (e & 511u) * 16u, wv[j]);
   }
+}
+template <int NT>
+__device__ __forceinline__ void stage_flow(const GcmArgs& a) {
+  stage_flow_tables<NT>(a);
   __syncthreads();
 }
 
@@ -559,10 +565,11 @@ __device__ __forceinline__ u32x4 flow_tree_r4(u32x4 acc, uint32_t lane) {
 // vs 19.3 us, of which the stream write alone costs 7.7 us per call (profiles/r05j_*, r05k_*).)
 // Unit u = (record r, chunk i) of a flow decomposition: chunk 0 absorbs the remainder (r0 X-blocks,
 // ceil(r0/64) steps), the others are C = 64·S X-blocks; returns the base X position of lane 0's
-// first step.
+// first step.  sep: the X-sequence is the data blocks only (the resident service: the length
+// block and E_K(J0) are another wave's, flow_unit<.., SEP>).
 __device__ __forceinline__ int32_t flow_unit_base(const GcmArgs& a, uint32_t u, uint32_t& r, uint32_t& i,
-                                                  uint32_t& steps) {
-  const int32_t nx = (int32_t)a.nb + 1, C = 64 * (int32_t)a.S;
+                                                  uint32_t& steps, bool sep = false) {
+  const int32_t nx = (int32_t)a.nb + (sep ? 0 : 1), C = 64 * (int32_t)a.S;
   r = u / a.nch;
   i = u - r * a.nch;
   steps = i == 0u ? (a.r0 + 63u) >> 6 : a.S;
@@ -583,15 +590,18 @@ __device__ __forceinline__ u32x4 flow_load_x(const GcmArgs& a, const uint8_t* in
 // a.chw, E_K(J0) folded into chunk 0) or V·H (device-keyed: E_K(J0) to a.ekj0).  va, vb: the
 // unit's first two input rows when `pre` (requested before the table staging).  Returns the
 // weighted partial (every lane), r = the unit's record.
-template <bool DECRYPT, bool DK>
+// SEP (the resident service, host-keyed): the chunks cover the data blocks only, chunk weights
+// H^(2 + (nch-1-i)C); the length block (L·H) and E_K(J0) are added by another wave (svc_j0_wave),
+// so a chunk of 64·S blocks is exactly S steps — chunk 0 no longer runs a near-empty extra step.
+template <bool DECRYPT, bool DK, bool SEP = false>
 __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk, const RowLanes& rl, u32x4 lenblk,
                                            uint32_t u, bool pre, u32x4 va, u32x4 vb, uint32_t& r) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nb = a.nb;
-  const int32_t nx = (int32_t)nb + 1;
+  const int32_t nx = (int32_t)nb + (SEP ? 0 : 1);
   const uint32_t rem = a.len - 16u * (nb ? nb - 1u : 0u);
   uint32_t i, steps;
-  const int32_t base = flow_unit_base(a, u, r, i, steps);
+  const int32_t base = flow_unit_base(a, u, r, i, steps, SEP);
   const uint8_t* in_rec = a.in + (uint64_t)r * a.in_stride;
   uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
   uint32_t n0, n1, n2;
@@ -626,7 +636,7 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
         store_partial(op, o, rem);
         x = DECRYPT ? pp : o;
       }
-    } else if (p == nx - 1) {
+    } else if (!SEP && p == nx - 1) {
       x = lenblk;
     }
     if (k == 0u) acc = x;  // wave-uniform; acc was 0
@@ -649,7 +659,7 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
   // r0 = G..2G-1 leading positions, so its first step is partial whenever 64 does not divide
   // r0 (1 MiB: 257 positions, lane 63 alone): lane 0 is idle there and encrypts J0 in that
   // step instead of the wave paying a whole AES pass for it afterwards.
-  const bool j0_step0 = i == 0u && base < 0;
+  const bool j0_step0 = !SEP && i == 0u && base < 0;
   u32x4 ekj = {0u, 0u, 0u, 0u};
   for (uint32_t k = 0; k < steps; k += 2u) {
     rotate_prio(it++);
@@ -662,7 +672,8 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
     if (k + 1u < steps) consume_ks(k + 1u, vb, keystream(ctr_of(k + 1u)));
     vb = prefetch(k + 3u);
   }
-  if (!j0_step0) ekj = i == 0u ? keystream(1u) : u32x4{0u, 0u, 0u, 0u};
+  if (SEP) ekj = u32x4{0u, 0u, 0u, 0u};
+  else if (!j0_step0) ekj = i == 0u ? keystream(1u) : u32x4{0u, 0u, 0u, 0u};
   if (pre) CMPI_PROBE(a, 2u);
   ustamp(30u);  // all steps done
   u32x4 V = flow_tree_r4(acc, lane);

@@ -107,7 +107,8 @@ void svc_release(Svc& S) {
   S.ev = nullptr;
 }
 
-// H^(1 + (63-k)·64·2^s) at wts[256s + 4k + 3] (the flow kernel's chunk-weight slot layout)
+// H^(2 + (63-k)·64·2^s) at wts[256s + 4k + 3] (the flow kernel's chunk-weight slot layout; the
+// service's chunks cover the data blocks only, the length block is the J0 wave's L·H)
 int svc_weights(const cmpi_ctx* c, Svc& S) {
   if (c->alg != CMPI_AES_128_GCM) {  // counter-mode service: no GHASH
     S.wts_ok = true;
@@ -116,7 +117,7 @@ int svc_weights(const cmpi_ctx* c, Svc& S) {
   std::vector<Blk> w(4 * 64 * 4);
   for (uint32_t s = 0; s < 4; ++s) {
     const Blk P = cmpi::gf_pow(c->H, 64u << s);
-    Blk wi = c->H;  // k = 63 down to 0
+    Blk wi = cmpi::gf_mul(c->H, c->H);  // k = 63 down to 0
     for (uint32_t k = 64; k-- > 0;) {
       w[256 * s + 4 * k + 3] = wi;
       wi = cmpi::gf_mul(wi, P);

@@ -23,11 +23,14 @@
 //   others: poll the 13 units (agent-scope loads, all in flight together) until every unit
 //           carries one seq != the last one seen and the generation unit names theirs; run their
 //           share, exit on STOP.
-//   message: the flow decomposition (gcm_flow_kernel's unit code): chunks of C = 64·S X-blocks,
-//           S the smallest power of two <= 8 with at most 64 chunks, one wavefront per chunk,
-//           8 chunks per workgroup; every chunk's partial is weighted by H^(1 + (nch-1-i)C) (host
-//           precomputed for the four S) and chunk 0 holds E_K(J0), so the tag is the XOR of the
-//           partials.  A workgroup XORs its waves' partials; with several workgroups each
+//   message: the flow decomposition (gcm_flow_kernel's unit code) over the DATA blocks: chunks of
+//           C = 64·S blocks, S the smallest power of two <= 8 with at most 64 chunks, one wavefront
+//           per chunk, 8 chunks per workgroup; every chunk's partial is weighted by
+//           H^(2 + (nch-1-i)C) (host precomputed for the four S), and a ninth wave of workgroup 0
+//           adds E_K(J0) ^ L·H (the length block), so the tag is the XOR of the partials and a
+//           chunk of 64·S blocks is S steps (round 5: with the length block and J0 in chunk 0 it
+//           ran a near-empty extra step, ~2.5 us of every message of a multiple of 1 KiB).
+//           A workgroup XORs its waves' partials; with several workgroups each
 //           publishes its partial write-through, writes its L2 back to the host (system release)
 //           and adds to an arrival counter — the last arriver XORs the partials
 //           (MI355X_MICROARCH.md, Valid forms: sc1 16-B stores, agent add, sc1 loads by the adder
@@ -50,9 +53,10 @@
 namespace cmpi {
 namespace dev {
 
-constexpr uint32_t kSvcThreads = 512u;
+constexpr uint32_t kSvcChunkWaves = 8u;  // chunk waves per workgroup
+constexpr uint32_t kSvcThreads = 576u;   // + the J0 wave (svc_j0_wave; idle in workgroups > 0)
 constexpr uint32_t kSvcGroups = 8u;      // workgroups (one per XCD when the chip is free)
-constexpr uint32_t kSvcMaxChunks = 64u;  // kSvcGroups x 8 waves
+constexpr uint32_t kSvcMaxChunks = 64u;  // kSvcGroups x kSvcChunkWaves
 constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u, kSvcXor = 3u, kSvcCtr = 4u, kSvcEcb = 5u;
 // descriptor words: op, len, in lo/hi, out lo/hi, then the op's own: GCM nonce[3] at 6..8, XOR
 // mask lo/hi at 6..7, CTR counter block as big-endian halves hi lo/hi, lo lo/hi at 8..11
@@ -69,7 +73,7 @@ struct SvcArgs {
   uint32_t* go;          // device: [16] arrival counter, [32..63] partials, [64..89] 13 published units {seq, word}
   uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
   u32x4* part;           // device: one partial per workgroup
-  const u32x4* wts;      // device: 4 x 64 x 4; wts[256s + 4k + 3] = H^(1 + (63-k)·64·2^s)
+  const u32x4* wts;      // device: 4 x 64 x 4; wts[256s + 4k + 3] = H^(2 + (63-k)·64·2^s)
   const uint32_t* te0;
   const u32x4* wtab;     // the ten flow nibble tables (DevTables::fnib); null for CTR / ECB contexts
   uint32_t seq0;         // last seq consumed before this launch
@@ -160,7 +164,7 @@ __device__ __forceinline__ bool svc_take(const uint32_t* go, uint32_t cur, uint3
 
 // LDS words shared by the workgroup (inside the flow aggregation area)
 constexpr uint32_t kSvcX = kFlowAgg + 256u;  // [0] exit, [1] seq, [2..13] descriptor, [14] last, [15] ok
-constexpr uint32_t kSvcTag = kFlowAgg + 128u;  // the XOR of the partials (16 B)
+constexpr uint32_t kSvcTag = kFlowAgg + 320u;  // the XOR of the partials (16 B; wave slots 0..8 below it)
 
 // A 64-bit address from two LDS words (lo, hi), wave-uniform.  readfirstlane returns int: each
 // word is taken as uint32_t before widening (a sign-extended low word with bit 31 set would put
@@ -171,21 +175,29 @@ __device__ __forceinline__ uint64_t lds_ptr64(uint32_t off) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Chunk plan of a message of `len` bytes: C = 64·2^ls X-blocks per chunk, nch chunks (chunk 0
+// Chunk plan of a message of `len` bytes: C = 64·2^ls data blocks per chunk, nch chunks (chunk 0
 // takes the remainder), ngrp workgroups of 8 chunks.
 __device__ __forceinline__ uint32_t svc_plan(uint32_t len, uint32_t& ls, uint32_t& nch, uint32_t ls_min = 0u) {
-  const uint32_t nx = ((len + 15u) >> 4) + 1u;
+  const uint32_t nx = (len + 15u) >> 4;
   ls = ls_min;
   while (ls < 3u && nx >= (kSvcMaxChunks + 1u) * (64u << ls)) ++ls;
   const uint32_t C = 64u << ls;
   nch = nx >= C ? nx / C : 1u;
-  return (nch + kSvcThreads / 64u - 1u) / (kSvcThreads / 64u);
+  return (nch + kSvcChunkWaves - 1u) / kSvcChunkWaves;
+}
+
+// E_K(J0) ^ L·H: the length block's GHASH term (weight H^1) and the tag mask, the part of the tag
+// no chunk holds (flow_unit<.., SEP>).  Every lane computes it; lane 0's copy is used.
+__device__ __forceinline__ u32x4 svc_j0_wave(const GcmArgs& a, const RoundKeys& rk, const RowLanes& rl, u32x4 lenblk) {
+  uint32_t w0 = a.nfix[0], w1 = a.nfix[1], w2 = a.nfix[2], w3 = __builtin_bswap32(1u);
+  aes128_enc(rk, rl, w0, w1, w2, w3);
+  return u32x4{w0, w1, w2, w3} ^ gmul_nib(lenblk, flow_tab(0u));
 }
 
 template <bool DECRYPT>
 __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl, uint32_t seq) {
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, wg = blockIdx.x;
-  constexpr uint32_t wpb = kSvcThreads / 64u;
+  constexpr uint32_t wpb = kSvcChunkWaves;
   const uint32_t len = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 12u));
   uint8_t* inp = reinterpret_cast<uint8_t*>(lds_ptr64(kSvcX + 16u));
   uint8_t* outp = reinterpret_cast<uint8_t*>(lds_ptr64(kSvcX + 24u));
@@ -199,14 +211,14 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   a.nfix[0] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 32u));
   a.nfix[1] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 36u));
   a.nfix[2] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 40u));
-  const uint32_t nx = a.nb + 1u;
+  const uint32_t nx = a.nb;  // data blocks (the X-sequence less its length block)
   uint32_t ls, nch;  // chunk 0: C <= r0 < 2C (or the whole message)
   const uint32_t ngrp = svc_plan(len, ls, nch, s.ls_min);  // workgroups with chunks
   const uint32_t C = 64u << ls;
   a.S = 1u << ls;
   a.nch = nch;
   a.r0 = nx - (nch - 1u) * C;
-  a.chw = s.wts + 256u * ls + 4u * (kSvcMaxChunks - nch);  // a.chw[4i + 3] = H^(1 + (nch-1-i)C)
+  a.chw = s.wts + 256u * ls + 4u * (kSvcMaxChunks - nch);  // a.chw[4i + 3] = H^(2 + (nch-1-i)C)
 #if CMPI_TOOLS
   a.unit_stamps = s.probe ? s.probe + 32u * (seq & 7u) : nullptr;
 #endif
@@ -216,9 +228,11 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   const uint32_t u = wg * wpb + wv;
   if (threadIdx.x == 0u) SVC_STAMP(s, seq, 2u + wg);
   u32x4 pw = {0u, 0u, 0u, 0u};
-  if (u < nch) {
+  if (wv == wpb) {  // the J0 wave (workgroup 0's)
+    if (wg == 0u) pw = svc_j0_wave(a, s.rk, rl, lenblk);
+  } else if (u < nch) {
     uint32_t r;
-    pw = flow_unit<DECRYPT, false>(a, s.rk, rl, lenblk, u, false, pw, pw, r);
+    pw = flow_unit<DECRYPT, false, true>(a, s.rk, rl, lenblk, u, false, pw, pw, r);
   }
   if (lane == 0u) lds_st128(kFlowAgg + 16u * wv, pw);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores are performed
@@ -226,7 +240,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   if (threadIdx.x == 0u) {
     SVC_STAMP(s, seq, 10u + wg);
     u32x4 x = lds128(kFlowAgg);
-    for (uint32_t j = 1; j < wpb; ++j) x ^= lds128(kFlowAgg + 16u * j);
+    for (uint32_t j = 1; j <= wpb; ++j) x ^= lds128(kFlowAgg + 16u * j);
     uint32_t last = 1u;
     if (ngrp > 1u) {
       wt_store16(s.part + wg, x);
@@ -343,7 +357,8 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
     GcmArgs t{};
     t.te0 = s.te0;
     t.wtab = s.wtab;
-    stage_flow<kSvcThreads>(t);
+    if (threadIdx.x < 512u) stage_flow_tables<512>(t);
+    __syncthreads();
   } else {  // CTR / ECB contexts: the AES rows only
     stage_rows(s.te0, kGcmRows);
     __syncthreads();
