@@ -450,10 +450,11 @@ def lds_roofline(w, kern_ms: float, device: int) -> dict:
 
 def copy_peak_gbs(device: int, nbytes: int = 1 << 30, reps: int = 10) -> float:
     """Achievable HBM bandwidth on this box: device-to-device copy of 1 GiB by the library's
-    streaming copy kernel (cmpi_debug_copy: 16 B per lane, four loads in flight, non-temporal;
-    the guide's float4 copy measures 6.29 TB/s) — read + write bytes / time, best of `reps` —
-    the 'measured copy-kernel peak' of BASELINE.md §3.  (Round 4 timed a torch uint8 copy_,
-    4.9 TB/s, which overstated frac_measured.)"""
+    streaming copy kernel (cmpi_debug_copy: 16 B per lane, grid-stride, 4 workgroups per CU — the
+    fastest of 80 forms swept in round 5, 5.6-5.7 TB/s, profiles/r05u_copy_probe2.jsonl; the
+    guide's float4 copy measures 6.29 TB/s) — read + write bytes / time, best of `reps` — the
+    'measured copy-kernel peak' of BASELINE.md §3.  (Round 4 timed a torch uint8 copy_, 4.9 TB/s,
+    which overstated frac_measured.)"""
     from cryptmpi_2022_amd import _native as N
 
     src = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", device))
@@ -1406,6 +1407,10 @@ def main() -> None:
             peak_meas = copy_peak_gbs(local)
             result["roofline"]["peak_measured"] = round(peak_meas, 1)
             result["roofline"]["frac_measured"] = round(achieved / peak_meas, 4)
+            result["roofline"]["peak_measured_note"] = (
+                "library copy kernel (16 B per lane, grid-stride, 4 workgroups per CU), best of 80 copy "
+                "forms swept on this hardware in round 5 (5.6-5.7 TB/s, profiles/r05u_copy_probe2.jsonl); "
+                "below the guide's 6.29 TB/s float4 copy: no form reached 6.0 TB/s here")
         except Exception as e:  # report, never hide
             result["roofline"]["peak_measured"] = {"error": repr(e)}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:

@@ -1446,14 +1446,14 @@ void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 |
 // event's fence writes back and invalidates the caches and leaves a ~6 us bubble before the
 // next launch — the bench times kernels with these instead.
 int cmpi_debug_copy(void* dst, const void* src, size_t n, void* stream) {
-  if (!dst || !src || n % 64 || ((uintptr_t)dst | (uintptr_t)src) % 16) return fail(CMPI_EINVAL, "copy: n % 64 / alignment");
+  if (!dst || !src || n % 16 || ((uintptr_t)dst | (uintptr_t)src) % 16) return fail(CMPI_EINVAL, "copy: n % 16 / alignment");
   if (n == 0) return CMPI_OK;
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   int ncu = 256;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
   const uint64_t nv = n / 16u;
-  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((nv / 4u + 255u) / 256u, (uint64_t)ncu * 16u));
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((nv + 255u) / 256u, (uint64_t)ncu * 4u));
   HIP_TRY(launch_k(cmpi::dev::copy16_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
                    reinterpret_cast<u32x4*>(dst), reinterpret_cast<const u32x4*>(src), nv));
   return CMPI_OK;

@@ -151,17 +151,15 @@ __global__ __launch_bounds__(256) void xor_bytes_kernel(uint8_t* out, const uint
 }
 
 // Streaming device copy (the measured HBM peak of bench.py's roofline, cmpi_debug_copy): 16 B
-// per lane, four loads in flight per lane before their stores, non-temporal both ways, a
-// grid-stride loop over the four quarters of the buffer.  nv = 16-byte units, a multiple of 4.
+// per lane, one load in flight per lane, plain loads and stores, a grid-stride loop run by 1 024
+// workgroups of 256 threads (4 per CU).  The fastest of 80 forms measured on 1 GiB
+// (tools/probe/copy_probe*.hip, profiles/r05e_copy_probe.jsonl, r05u_copy_probe2.jsonl: 5.71 TB/s
+// read + write; 2 loads in flight, non-temporal stores, per-workgroup chunks, 512 / 1 024-thread
+// workgroups and 256 - 16 384 workgroups all 1-15 % slower — the round's first form, four
+// non-temporal loads per lane over 4 096 workgroups, ran 4.3 TB/s).
 __global__ __launch_bounds__(256) void copy16_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src, uint64_t nv) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, q = nv / 4u;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < q; i += stride) {
-    u32x4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(src + i + (uint64_t)k * q);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v[k], dst + i + (uint64_t)k * q);
-  }
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) dst[i] = src[i];
 }
 
 }  // namespace dev

@@ -606,7 +606,12 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
   uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
   uint32_t n0, n1, n2;
   gcm_nonce(a, r, !DECRYPT && i == 0u && lane == 0u, n0, n1, n2);
-  auto prefetch = [&](uint32_t k) -> u32x4 { return flow_load_x(a, in_rec, base, k, rem); };
+  // input rows of steps beyond the unit's own are not loaded (wave-uniform): they are the next
+  // chunk's blocks — L2 re-reads on device records, a second PCIe read of them on the service's
+  // host messages
+  auto prefetch = [&](uint32_t k) -> u32x4 {
+    return k < steps ? flow_load_x(a, in_rec, base, k, rem) : u32x4{0u, 0u, 0u, 0u};
+  };
   CtrCache cc;
   uint32_t cc_win = 0xffffffffu;
   auto keystream = [&](uint32_t ctr) -> u32x4 {
@@ -708,7 +713,7 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       uint32_t r, i, steps;
       const int32_t base = flow_unit_base(a, u, r, i, steps);
       va0 = flow_load_x(a, a.in + (uint64_t)r * a.in_stride, base, 0u, rem);
-      vb0 = flow_load_x(a, a.in + (uint64_t)r * a.in_stride, base, 1u, rem);
+      if (steps > 1u) vb0 = flow_load_x(a, a.in + (uint64_t)r * a.in_stride, base, 1u, rem);
     }
   }
   stage_flow<NT>(a);

@@ -43,9 +43,10 @@ struct Svc {
   int dev = 0, slot = 0;
   hipEvent_t ev = nullptr;     // recorded after this service's last launch
   bool launched = false;
-  uint32_t* hw = nullptr;      // page-locked coherent: ring [0..15] (four 16-B chunks), kick [16], done [32..44]
+  uint32_t* hw = nullptr;      // page-locked coherent (kSvcHostBytes): ring [0..15] (four 16-B chunks), kick [16],
+                               // exit word [20], completion slots [64 + 8w .. 64 + 8w + 7] of workgroups w < 8
   uint32_t* dw = nullptr;      // its device address
-  uint32_t* go = nullptr;      // device control area: counter (at +64), partials (at +128), published units (at +256)
+  uint32_t* go = nullptr;      // device control area: published units (at +256)
   cmpi::dev::u32x4* wts = nullptr;  // device chunk weights (4 x 64 x 4 blocks)
   bool wts_ok = false;
   uint8_t* bounce = nullptr;   // page-locked: pageable messages
@@ -54,10 +55,24 @@ struct Svc {
   uint32_t gen = 0;            // generation of the last launch
   bool running = false;
   uint32_t idle_us = 2000;
+  uint32_t ls_min = 0;         // the running generation's chunk-plan floor (SvcArgs::ls_min)
   uint32_t* ring() { return hw; }
   uint32_t* kick() { return hw + 16; }
-  uint32_t* done() { return hw + 32; }
+  uint32_t* exited() { return hw + 20; }
+  uint32_t* done() { return hw + 64; }
 };
+constexpr size_t kSvcHostBytes = 1024;
+
+// Workgroups that serve a message of `len` bytes (service_kernels.hpp svc_plan; each posts a
+// completion slot): GCM messages by the chunk plan, counter-mode ops by the leader alone.
+uint32_t svc_groups(uint32_t op, size_t len, uint32_t ls_min) {
+  if (op != cmpi::dev::kSvcSeal && op != cmpi::dev::kSvcOpen) return 1;
+  const uint32_t nx = (uint32_t)((len + 15) >> 4);
+  uint32_t ls = ls_min;
+  while (ls < 3u && nx >= (cmpi::dev::kSvcMaxChunks + 1u) * (64u << ls)) ++ls;
+  const uint32_t C = 64u << ls, nch = nx >= C ? nx / C : 1u;
+  return (nch + cmpi::dev::kSvcChunkWaves - 1u) / cmpi::dev::kSvcChunkWaves;
+}
 
 // This service's last generation has left the device (its stream slot may already run another
 // context's generation behind it).
@@ -82,6 +97,7 @@ constexpr size_t kSvcWtsBytes = 4 * 64 * 4 * 16;
 void svc_wipe(Svc& S) {
   wipe_dev(S.wts, kSvcWtsBytes);
   wipe_dev(S.go, cmpi::dev::kSvcGoBytes);
+  if (S.hw) memset(S.done(), 0, 4 * 8 * cmpi::dev::kSvcGroups);  // the last message's partials
   if (S.bounce) memset(S.bounce, 0, S.bcap);
   S.wts_ok = false;
   wipe_sync();  // svc_weights' next upload must land after the wipe
@@ -141,7 +157,7 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
     std::unique_lock<std::mutex> t(svc_slot(S.dev, i).m);
     const SvcSlot& c_sl = svc_slot(S.dev, i);
     Svc* o = c_sl.owner;
-    if (!o || o == &S || __atomic_load_n(o->done() + 12, __ATOMIC_ACQUIRE) == c_sl.owner_gen) {
+    if (!o || o == &S || __atomic_load_n(o->exited(), __ATOMIC_ACQUIRE) == c_sl.owner_gen) {
       S.slot = i;
       g = std::move(t);
       break;
@@ -158,15 +174,14 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
   cmpi::dev::SvcArgs a{};
   a.ring = S.dw;
   a.kick = S.dw + 16;
-  a.done = S.dw + 32;
+  a.exited = S.dw + 20;
+  a.done = S.dw + 64;
   a.go = S.go;
-  a.cnt = S.go + 16;
-  a.part = reinterpret_cast<cmpi::dev::u32x4*>(S.go + 32);
   a.wts = S.wts;
   a.te0 = c->dt->te0;
   a.wtab = c->alg == CMPI_AES_128_GCM ? reinterpret_cast<const cmpi::dev::u32x4*>(c->dt->fnib[0]) : nullptr;
   a.seq0 = seq0;
-  a.ls_min = (uint32_t)g_svc_ls_min.load();
+  a.ls_min = S.ls_min = (uint32_t)g_svc_ls_min.load();
   a.gen = ++S.gen;
   a.idle_ticks = (uint64_t)S.idle_us * 100u;
   a.life_ticks = kSvcLifeUs * 100u;
@@ -175,7 +190,6 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
 #if CMPI_TOOLS
   a.probe = g_svc_probe.load();
 #endif
-  HIP_TRY(hipMemsetAsync(S.go + 16, 0, 4, S.st));  // arrival counter
   void* kargs[] = {&a};
   HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(cmpi::dev::gcm_service_kernel), dim3(cmpi::dev::kSvcGroups),
                           dim3(cmpi::dev::kSvcThreads), kargs, cmpi::dev::kFlowLds, S.st));
@@ -188,17 +202,21 @@ int svc_launch(const cmpi_ctx* c, Svc& S, uint32_t seq0) {
 }
 
 // The current generation has exited (idle, lifetime, stop): its exit word is written.
-bool svc_exited(Svc& S) { return __atomic_load_n(S.done() + 12, __ATOMIC_ACQUIRE) == S.gen; }
+bool svc_exited(Svc& S) { return __atomic_load_n(S.exited(), __ATOMIC_ACQUIRE) == S.gen; }
 
-// Completion of message `seq`: all five {seq, word} pairs (status, tag words 0-3) carry it; each
-// pair is read as one 8-byte load, so its word belongs to its seq.  w[0] = status, w[1..4] = tag.
-bool svc_done(Svc& S, uint32_t seq, uint32_t (&w)[5]) {
+// Completion of message `seq`: the slots of its ngrp workgroups carry it in all four {seq, word}
+// pairs (each read as one 8-byte load, so its word belongs to its seq); x = the XOR of their
+// partials (a GCM message's tag).
+bool svc_done(Svc& S, uint32_t seq, uint32_t ngrp, uint32_t (&x)[4]) {
   const uint64_t* p = reinterpret_cast<const uint64_t*>(S.done());
-  for (int i = 0; i < 5; ++i) {
-    const uint64_t v = __atomic_load_n(p + i, __ATOMIC_ACQUIRE);
-    if ((uint32_t)v != seq) return false;
-    w[i] = (uint32_t)(v >> 32);
-  }
+  uint32_t t[4] = {0, 0, 0, 0};
+  for (uint32_t w = 0; w < ngrp; ++w)
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t v = __atomic_load_n(p + 4 * w + i, __ATOMIC_ACQUIRE);
+      if ((uint32_t)v != seq) return false;
+      t[i] ^= (uint32_t)(v >> 32);
+    }
+  memcpy(x, t, sizeof t);
   return true;
 }
 
@@ -226,8 +244,8 @@ int svc_shutdown_locked(cmpi_ctx* c) {
 }
 
 // Post descriptor d as the next message (the service launched first if it is not running) and
-// wait for its completion words w (status, tag 0-3).  hmu held.
-int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc], uint32_t (&w)[5]) {
+// wait for its workgroups' completion slots; w = the XOR of their partials.  hmu held.
+int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc], uint32_t (&w)[4]) {
   if (S.running && svc_exited(S)) {  // idled out (or kicked) since the last message
     if (int rc = svc_drain(S)) return rc;
     S.running = false;
@@ -236,14 +254,15 @@ int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc]
     if (int rc = svc_launch(c, S, S.seq)) return rc;
   const uint32_t seq = ++S.seq;
   svc_post(S, d, seq);
+  const uint32_t ngrp = svc_groups(d[0], d[1], S.ls_min);
   const auto t0 = std::chrono::steady_clock::now();
   int relaunches = 0;
   for (uint32_t i = 1;; ++i) {
-    if (svc_done(S, seq, w)) break;
+    if (svc_done(S, seq, ngrp, w)) break;
     if (svc_exited(S)) {  // the generation ended (lifetime, kick): let every workgroup finish first
       if (int rc = svc_drain(S)) return rc;
       S.running = false;
-      if (svc_done(S, seq, w)) break;
+      if (svc_done(S, seq, ngrp, w)) break;
       if (++relaunches > 2) return fail(CMPI_EHIP, "message service did not complete message %u", seq);
       if (int rc = svc_launch(c, S, seq - 1)) return rc;  // it never saw the message
       continue;
@@ -251,7 +270,7 @@ int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc]
     if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
       const hipError_t e = hipEventQuery(S.ev);  // this generation (the slot's stream may hold others)
       if (e != hipSuccess && e != hipErrorNotReady) return fail(CMPI_EHIP, "service kernel: %s", hipGetErrorString(e));
-      if (e == hipSuccess && !svc_done(S, seq, w) && !svc_exited(S))
+      if (e == hipSuccess && !svc_done(S, seq, ngrp, w) && !svc_exited(S))
         return fail(CMPI_EHIP, "service kernel ended without completing message %u", seq);
     }
   }
@@ -301,15 +320,22 @@ int svc_call(const cmpi_ctx* c, Svc& S, uint8_t* out, const uint8_t* in, const u
                                      (uint32_t)(uintptr_t)dout,
                                      (uint32_t)((uintptr_t)dout >> 32)};
   memcpy(d + 6, nonce, 12);
-  uint32_t w[5];
-  if (int rc = svc_exec(c, S, d, w)) return rc;
-  const int32_t ok = (int32_t)w[0];
-  if (hout) memcpy(out, hout, len);
-  if (!DEC) memcpy(out + len, w + 1, 16);  // the tag travels in the completion words
-  if (DEC) {
-    if (status) *status = ok;
-    if (ok != 1) return fail(CMPI_EAUTH, "1 of 1 records failed authentication");
+  uint32_t tag[4];
+  if (int rc = svc_exec(c, S, d, tag)) return rc;  // the tag: the XOR of the workgroups' partials
+  if (!DEC) {
+    if (hout) memcpy(out, hout, len);
+    memcpy(out + len, tag, 16);
+    return CMPI_OK;
   }
+  uint8_t diff = 0;  // the received tag vs the computed one, every byte compared
+  for (int i = 0; i < 16; ++i) diff |= in[len + i] ^ reinterpret_cast<const uint8_t*>(tag)[i];
+  const int32_t ok = diff == 0 ? 1 : 0;
+  if (status) *status = ok;
+  if (!ok) {  // a forged message's plaintext is zero-filled (aead.h:276-278)
+    memset(out, 0, len);
+    return fail(CMPI_EAUTH, "1 of 1 records failed authentication");
+  }
+  if (hout) memcpy(out, hout, len);
   return CMPI_OK;
 }
 
@@ -335,7 +361,7 @@ int svc_stream(const cmpi_ctx* c, Svc& S, uint32_t op, uint8_t* out, const uint8
     d[10] = (uint32_t)l;
     d[11] = (uint32_t)(l >> 32);
   }
-  uint32_t w[5];
+  uint32_t w[4];
   return svc_exec(c, S, d, w);
 }
 
@@ -384,7 +410,7 @@ int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
   S.dev = c->device;
   S.slot = (int)(g_svc_next_slot[c->device].fetch_add(1) % kSvcSlots);
   if (hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void**)&S.hw, 256, hipHostMallocCoherent) != hipSuccess ||
+      hipHostMalloc((void**)&S.hw, kSvcHostBytes, hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&S.dw, S.hw, 0) != hipSuccess || hipMalloc((void**)&S.go, cmpi::dev::kSvcGoBytes) != hipSuccess ||
       hipMalloc((void**)&S.wts, kSvcWtsBytes) != hipSuccess || hipMemset(S.go, 0, cmpi::dev::kSvcGoBytes) != hipSuccess) {
     svc_release(S);
@@ -392,7 +418,7 @@ int cmpi_service_start(cmpi_ctx* c, uint32_t idle_us) {
     c->svc = nullptr;
     return fail(CMPI_EHIP, "message service allocation failed");
   }
-  memset(S.hw, 0, 256);
+  memset(S.hw, 0, kSvcHostBytes);
   return CMPI_OK;
 }
 

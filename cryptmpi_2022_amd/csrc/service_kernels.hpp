@@ -17,8 +17,8 @@
 //           seqlock's three drains and the readers' two-phase reads took 1.7 + 1.5 us of each
 //           64 KiB message, tools/svc_timeline.py);
 //           on idle / lifetime / op STOP / a kick (the host word kick == gen: another context's
-//           service takes this stream slot) it publishes a STOP descriptor, writes done[12] = gen
-//           and exits.  A message whose chunks fit one workgroup is served by the leader's
+//           service takes this stream slot) it publishes a STOP descriptor, writes the exit word
+//           (= gen) and exits.  A message whose chunks fit one workgroup is served by the leader's
 //           workgroup alone and not published.
 //   others: poll the 13 units (agent-scope loads, all in flight together) until every unit
 //           carries one seq != the last one seen and the generation unit names theirs; run their
@@ -30,21 +30,19 @@
 //           adds E_K(J0) ^ L·H (the length block), so the tag is the XOR of the partials and a
 //           chunk of 64·S blocks is S steps (round 5: with the length block and J0 in chunk 0 it
 //           ran a near-empty extra step, ~2.5 us of every message of a multiple of 1 KiB).
-//           A workgroup XORs its waves' partials; with several workgroups each
-//           publishes its partial write-through, writes its L2 back to the host (system release)
-//           and adds to an arrival counter — the last arriver XORs the partials
-//           (MI355X_MICROARCH.md, Valid forms: sc1 16-B stores, agent add, sc1 loads by the adder
-//           whose add came last), checks the tag (open; zero-fills a forged message,
-//           aead.h:276-278), resets the counter, and after a system-scope release of the record
-//           bytes posts the completion as five 8-byte {seq, word} pairs (status, tag words 0-3) in
-//           three 16-byte system-scope stores: no store waits on another's PCIe acknowledgement,
-//           and the host takes a pair only with the new seq in it, so a pair cannot tear; the host
-//           writes a seal's tag into out + len itself.
+//           Every workgroup XORs its waves' partials and, after a system-scope release of its
+//           record bytes, posts its own completion slot: four 8-byte {seq, word} pairs (the
+//           partial) in two 16-byte system-scope stores — no cross-workgroup arrival (round 5:
+//           the agent-scope counter, the last arriver's partial reads and its second release were
+//           2.5 us of each multi-workgroup message).  The host takes a pair only with the new seq
+//           in it (a pair cannot tear), waits for the message's workgroups' slots, and XORs the
+//           partials into the tag: it writes a seal's tag into out + len and checks an open's
+//           (a forged message's plaintext is zero-filled, aead.h:276-278).
 //   counter-mode ops (CTR contexts: the 702 / 700 small-message XORs, send.c:1273-1465,
 //           recv.c:954-1023, :1187-1220): kSvcXor out = in ^ mask, kSvcCtr out = in ^ E_K(ctr + j),
 //           kSvcEcb out = E_K(in) per 16-byte block (the 602 sub-key K' = AES_K(V), send.c:583)
 //           (in null: the keystream), at most kSvcMaxStreamLen bytes, served by the leader's
-//           workgroup alone and completed like a seal (status 1, no tag).
+//           workgroup alone and completed like a one-workgroup seal (partial 0).
 // Every wave's wait loop is bounded by the wall clock: the grid drains even if the host vanishes.
 #pragma once
 #include "ctr_kernels.hpp"
@@ -69,10 +67,9 @@ constexpr uint32_t kSvcMaxStreamLen = 65536u;   // counter-mode ops: the 702 rin
 struct SvcArgs {
   const uint32_t* ring;  // page-locked host words (device address): chunks [4c] = seq, [4c+1..4c+3] = desc[3c..3c+2]
   const uint32_t* kick;  // page-locked host word: == gen asks this generation to exit (its stream slot is wanted)
-  uint32_t* done;        // page-locked host words: [0..9] five {seq, word} pairs (status, tag 0-3), [12] exited generation
-  uint32_t* go;          // device: [16] arrival counter, [32..63] partials, [64..89] 13 published units {seq, word}
-  uint32_t* cnt;         // device: arrival counter (0 between messages; zeroed before each launch)
-  u32x4* part;           // device: one partial per workgroup
+  uint32_t* done;        // page-locked host words: workgroup w's completion slot [8w .. 8w+7], four {seq, partial word} pairs
+  uint32_t* exited;      // page-locked host word: the generation that exited
+  uint32_t* go;          // device: [64..89] 13 published units {seq, word}
   const u32x4* wts;      // device: 4 x 64 x 4; wts[256s + 4k + 3] = H^(2 + (63-k)·64·2^s)
   const uint32_t* te0;
   const u32x4* wtab;     // the ten flow nibble tables (DevTables::fnib); null for CTR / ECB contexts
@@ -89,13 +86,15 @@ struct SvcArgs {
 // Diagnostics build only (-DCMPI_TOOLS=1, tools/svc_timeline.py): 100 MHz wall-clock stamps of a
 // message's phases into probe[32 * (seq % 8) + slot]: 0 the leader sees the seq in the host ring,
 // 1 the descriptor is in the leader workgroup's LDS (and published), 2 + wg a workgroup starts
-// the message, 10 + wg its waves' record stores are performed, 18 + wg its partial is published
-// and counted, 26 the last arriver has the tag / verdict, 27 the completion words are issued;
-// 28..31 workgroup 0's first unit: first keystream, first step consumed, steps done, tree + weight.
+// the message, 10 + wg its waves' record stores are performed, 18 + wg its completion slot is
+// issued; 28..31 workgroup 0's first unit: first keystream, first step consumed, steps done,
+// tree + weight.
 #if CMPI_TOOLS
 #define SVC_STAMP(s, seq, slot)                                                                       \
   do {                                                                                                \
-    if ((s).probe) (s).probe[32u * ((seq) & 7u) + (slot)] = wall_clock64();                           \
+    if ((s).probe) /* write-through: other XCDs' stamps reach memory while the kernel stays resident */  \
+      __hip_atomic_store((s).probe + 32u * ((seq) & 7u) + (slot), wall_clock64(), __ATOMIC_RELAXED,   \
+                         __HIP_MEMORY_SCOPE_AGENT);                                                   \
   } while (0)
 #else
 #define SVC_STAMP(s, seq, slot) \
@@ -116,25 +115,6 @@ __device__ __forceinline__ void sys_store16(uint32_t* p, u32x4 v) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(v, r, 0, 0, 17);
 }
-__device__ __forceinline__ uint32_t wt_load(const uint32_t* p) {  // write-through word (sc1)
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void wt_store(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 16 B published for other workgroups (two 8-B write-through stores) / read back
-__device__ __forceinline__ void wt_store16(u32x4* p, u32x4 v) {
-  uint64_t* q = reinterpret_cast<uint64_t*>(p);
-  __hip_atomic_store(q, (uint64_t)v[0] | ((uint64_t)v[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(q + 1, (uint64_t)v[2] | ((uint64_t)v[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u32x4 wt_load16(const u32x4* p) {
-  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
-  const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-}
-
 // The leader's descriptor for the other workgroups: units 0..11 = {seq, d[j]}, unit 12 = {seq, gen}.
 __device__ __forceinline__ void svc_publish(uint32_t* go, uint32_t seq, uint32_t gen, const uint32_t (&d)[kSvcDesc]) {
   uint64_t* u = reinterpret_cast<uint64_t*>(go + kSvcPubWords);
@@ -162,9 +142,15 @@ __device__ __forceinline__ bool svc_take(const uint32_t* go, uint32_t cur, uint3
   return true;
 }
 
+// Completion slot of a workgroup: four {seq, word} pairs (its partial) in two 16-byte system-scope
+// stores, neither waiting for the other's PCIe acknowledgement.
+__device__ __forceinline__ void svc_post(uint32_t* slot, uint32_t seq, u32x4 x) {
+  sys_store16(slot, u32x4{seq, x[0], seq, x[1]});
+  sys_store16(slot + 4, u32x4{seq, x[2], seq, x[3]});
+}
+
 // LDS words shared by the workgroup (inside the flow aggregation area)
-constexpr uint32_t kSvcX = kFlowAgg + 256u;  // [0] exit, [1] seq, [2..13] descriptor, [14] last, [15] ok
-constexpr uint32_t kSvcTag = kFlowAgg + 320u;  // the XOR of the partials (16 B; wave slots 0..8 below it)
+constexpr uint32_t kSvcX = kFlowAgg + 256u;  // [0] exit, [1] seq, [2..13] descriptor
 
 // A 64-bit address from two LDS words (lo, hi), wave-uniform.  readfirstlane returns int: each
 // word is taken as uint32_t before widening (a sign-extended low word with bit 31 set would put
@@ -241,52 +227,9 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
     SVC_STAMP(s, seq, 10u + wg);
     u32x4 x = lds128(kFlowAgg);
     for (uint32_t j = 1; j <= wpb; ++j) x ^= lds128(kFlowAgg + 16u * j);
-    uint32_t last = 1u;
-    if (ngrp > 1u) {
-      wt_store16(s.part + wg, x);
-      // whole record blocks are write-through stores the waves drained above (and the partial an
-      // agent-scope store): no L2 write-back before the add — only a message with a partial last
-      // block has plain byte stores to release (round 5: the fence was 1.7 us of each arrival)
-      if (len & 15u) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      last = __hip_atomic_fetch_add(s.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngrp - 1u ? 1u : 0u;
-      if (last) {
-        x = wt_load16(s.part);
-        for (uint32_t j = 1; j < ngrp; ++j) x ^= wt_load16(s.part + j);
-      }
-    }
-    lds_st32(kSvcX + 56u, last);
-    lds_st128(kSvcTag, x);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's record bytes reach the host first
+    svc_post(s.done + 8u * wg, seq, x);
     SVC_STAMP(s, seq, 18u + wg);
-  }
-  __syncthreads();
-  if (!lds32(kSvcX + 56u)) return;  // workgroup-uniform
-  // the last arriver: tag / verdict, then the host word
-  if (threadIdx.x == 0u) {
-    uint32_t ok = 1u;
-    if (DECRYPT) {
-      const u32x4 d = ld_blk(inp + len) ^ lds128(kSvcTag);
-      ok = (d[0] | d[1] | d[2] | d[3]) == 0u ? 1u : 0u;
-    }
-    lds_st32(kSvcX + 60u, ok);
-    SVC_STAMP(s, seq, 26u);
-  }
-  __syncthreads();
-  if (DECRYPT && !lds32(kSvcX + 60u)) {  // forged: zero-fill the plaintext (after every workgroup's stores)
-    const uint32_t full4 = len & ~3u;
-    for (uint32_t i = threadIdx.x * 4u; i < full4; i += kSvcThreads * 4u) *reinterpret_cast<u32a*>(outp + i) = 0u;
-    for (uint32_t i = full4 + threadIdx.x; i < len; i += kSvcThreads) outp[i] = 0u;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if (threadIdx.x == 0u) {
-    if (ngrp > 1u) wt_store(s.cnt, 0u);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the record bytes (every wave waited for its own) reach the host first
-    const u32x4 tag = DECRYPT ? u32x4{0u, 0u, 0u, 0u} : lds128(kSvcTag);
-    sys_store16(s.done, u32x4{seq, lds32(kSvcX + 60u), seq, tag[0]});
-    sys_store16(s.done + 4, u32x4{seq, tag[1], seq, tag[2]});
-    sys_store16(s.done + 8, u32x4{seq, tag[3], 0u, 0u});
-    SVC_STAMP(s, seq, 27u);
   }
 }
 
@@ -346,9 +289,7 @@ __device__ __forceinline__ void svc_stream_op(const SvcArgs& s, const RowLanes& 
   __syncthreads();
   if (threadIdx.x == 0u) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    sys_store16(s.done, u32x4{seq, 1u, seq, 0u});
-    sys_store16(s.done + 4, u32x4{seq, 0u, seq, 0u});
-    sys_store16(s.done + 8, u32x4{seq, 0u, 0u, 0u});
+    svc_post(s.done, seq, u32x4{0u, 0u, 0u, 0u});
   }
 }
 
@@ -438,7 +379,7 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
     cur = q;
     t_last = wall_clock64();
   }
-  if (leader && threadIdx.x == 0u) __hip_atomic_store(s.done + 12, s.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (leader && threadIdx.x == 0u) __hip_atomic_store(s.exited, s.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace dev

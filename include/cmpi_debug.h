@@ -31,8 +31,9 @@ void cmpi_debug_force_wide(int mode, uint32_t steps);
    writeback/invalidate when recorded).  event_ms: elapsed ms between two recorded events after
    the stream has been synchronised, -1 on error. */
 void* cmpi_debug_event_new(void);
-/* Streaming device-to-device copy of n bytes (n % 64 == 0, 16-byte aligned), asynchronous on
-   `stream`: bench.py's measured HBM peak (16 B per lane, 4 loads in flight, non-temporal). */
+/* Streaming device-to-device copy of n bytes (n % 16 == 0, 16-byte aligned), asynchronous on
+   `stream`: bench.py's measured HBM peak (16 B per lane, grid-stride over 4 workgroups per CU:
+   the fastest of the forms measured, ctr_kernels.hpp copy16_kernel). */
 int cmpi_debug_copy(void* dst, const void* src, size_t n, void* stream);
 int cmpi_debug_event_record(void* ev, void* stream);
 float cmpi_debug_event_ms(void* a, void* b);

@@ -185,3 +185,18 @@ def test_ocb_config3_sample():
     idx = torch.from_numpy(np.random.default_rng(3).choice(nrec, 256, replace=False)).cuda()
     want = oracle.ocb_seal_batch(KEY, nonces.view(nrec, 12)[idx].cpu().numpy(), pt.view(nrec, n)[idx].cpu().numpy())
     assert np.array_equal(ct.view(nrec, n + 16)[idx].cpu().numpy(), want)
+
+
+# ------------------------------------------------------------ the bench's copy kernel
+@pytest.mark.parametrize("n", [16, 4096, (1 << 20) + 48, 64 << 20])
+def test_debug_copy_kernel(n):
+    """cmpi_debug_copy (bench.py's measured HBM peak) copies every byte, grid-stride tail included."""
+    import torch
+
+    from cryptmpi_2022_amd import _native as N
+
+    src = dev(splitmix64_bytes(n, n))
+    dst = empty(n, fill=0)
+    N.check(N.lib().cmpi_debug_copy(dst.data_ptr(), src.data_ptr(), n, torch.cuda.current_stream().cuda_stream))
+    assert np.array_equal(host(dst)[:n], host(src)[:n])
+    assert N.lib().cmpi_debug_copy(dst.data_ptr(), src.data_ptr(), 8, None) != 0  # n % 16 refused

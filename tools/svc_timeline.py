@@ -8,10 +8,9 @@ Phases (us, medians over the messages; per-workgroup phases take the slowest wor
   wg_start    -> the last workgroup starts the message
   compute     workgroup start -> its waves' record stores performed (input read over PCIe, AES,
               lane tree, chunk weight, output written over PCIe)
-  arrive      -> its partial published and counted (agent-scope release + atomic)
-  finish      last arrival -> the last arriver has the tag / verdict
-  complete    -> the completion words are issued (system-scope release of the record bytes)
-  gpu_span    leader sees the seq -> completion issued
+  post        -> its completion slot issued (system-scope release of its record bytes + two
+              16-byte system-scope stores)
+  gpu_span    leader sees the seq -> the last workgroup's completion issued
   host_call   the host's time per call (post, wait for the completion word, tag copy)
 Run with the diagnostics library (make -C tools diag):  python tools/svc_timeline.py"""
 import json
@@ -74,14 +73,13 @@ def main():
                 ngrp = int(act[0].sum())
                 wg_start = np.where(act, start, -np.inf).max(axis=1)
                 comp = np.where(act, r[:, 10:18] - start, -np.inf).max(axis=1)
-                arr = np.where(act, r[:, 18:26], -np.inf).max(axis=1)
+                done = np.where(act, r[:, 18:26], -np.inf).max(axis=1)
                 med = lambda x: round(float(np.median(x)), 2)  # noqa: E731
                 res[f"{op}_{n}"] = {
                     "workgroups": ngrp, "messages": len(rows),
                     "publish": med(r[:, 1]), "wg_start": med(wg_start), "compute": med(comp),
-                    "arrive": med(arr - np.where(act, r[:, 10:18], -np.inf).max(axis=1)),
-                    "finish": med(r[:, 26] - arr), "complete": med(r[:, 27] - r[:, 26]),
-                    "gpu_span": med(r[:, 27]), "host_call": med(host),
+                    "post": med(np.where(act, r[:, 18:26] - r[:, 10:18], -np.inf).max(axis=1)),
+                    "gpu_span": med(done), "host_call": med(host),
                     # workgroup 0's first unit (chunk 0 on the single-workgroup shapes), from its start
                     "u_first_keystream": med(r[:, 28] - r[:, 2]), "u_first_step": med(r[:, 29] - r[:, 2]),
                     "u_steps_done": med(r[:, 30] - r[:, 2]), "u_tree_weight": med(r[:, 31] - r[:, 2]),
