@@ -585,6 +585,8 @@ struct NonceSpec {
   uint32_t fix[3] = {0, 0, 0};
 };
 
+bool is_pinned(const void* p);  // page-locked host memory (below)
+
 template <bool DEC>
 int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t* in, size_t in_stride,
               const uint8_t* nonces, size_t nonce_stride, size_t len, size_t nrec, int32_t* status,
@@ -662,10 +664,16 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     a.one_wg = one_wg ? 1u : 0u;
     if (one_wg && DEC && !status) a.status = reinterpret_cast<int32_t*>(ws + (size_t)nrec * p.nseg * 16);
     const bool dk = !a.chw;  // device-keyed context
-    const void* fn = NT == 512 ? (dk ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, true>)
-                                     : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 512, false>))
-                               : (dk ? reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, true>)
-                                     : reinterpret_cast<const void*>(cmpi::dev::gcm_flow_kernel<DEC, 1024, false>));
+    // records in host memory (the direct host paths: 602 outer messages, single messages without
+    // the service): units read only their own rows over PCIe
+    const bool hostin = NT == 512 && is_pinned(in);
+    using namespace cmpi::dev;
+    const void* fn = hostin ? (dk ? reinterpret_cast<const void*>(gcm_flow_kernel<DEC, 512, true, true>)
+                                  : reinterpret_cast<const void*>(gcm_flow_kernel<DEC, 512, false, true>))
+                   : NT == 512 ? (dk ? reinterpret_cast<const void*>(gcm_flow_kernel<DEC, 512, true>)
+                                     : reinterpret_cast<const void*>(gcm_flow_kernel<DEC, 512, false>))
+                               : (dk ? reinterpret_cast<const void*>(gcm_flow_kernel<DEC, 1024, true>)
+                                     : reinterpret_cast<const void*>(gcm_flow_kernel<DEC, 1024, false>));
     const size_t lds = (size_t)cmpi::dev::kFlowLds;
     if ((rc = set_lds_attr(fn, c->device, lds))) return rc;
     const uint32_t wpb = (uint32_t)NT / 64u;

@@ -593,7 +593,8 @@ __device__ __forceinline__ u32x4 flow_load_x(const GcmArgs& a, const uint8_t* in
 // SEP (the resident service, host-keyed): the chunks cover the data blocks only, chunk weights
 // H^(2 + (nch-1-i)C); the length block (L·H) and E_K(J0) are added by another wave (svc_j0_wave),
 // so a chunk of 64·S blocks is exactly S steps — chunk 0 no longer runs a near-empty extra step.
-template <bool DECRYPT, bool DK, bool SEP = false>
+// OWN: load only the unit's own input rows (records in host memory, read over PCIe).
+template <bool DECRYPT, bool DK, bool SEP = false, bool OWN = SEP>
 __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk, const RowLanes& rl, u32x4 lenblk,
                                            uint32_t u, bool pre, u32x4 va, u32x4 vb, uint32_t& r) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -606,11 +607,14 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
   uint8_t* out_rec = a.out + (uint64_t)r * a.out_stride;
   uint32_t n0, n1, n2;
   gcm_nonce(a, r, !DECRYPT && i == 0u && lane == 0u, n0, n1, n2);
-  // input rows of steps beyond the unit's own are not loaded (wave-uniform): they are the next
-  // chunk's blocks — L2 re-reads on device records, a second PCIe read of them on the service's
-  // host messages
+  // OWN (records in host memory: the service's messages, direct host paths): input rows of steps
+  // beyond the unit's own are not loaded (wave-uniform) — they are the next chunk's blocks, a
+  // second PCIe read of them (64 KiB served seal 13.9 -> 11.8 us).  On device records the same
+  // skip made the flow kernel slower (8 x 1 MiB seal 19.7 -> 20.4 us, open 20.2 -> 21.9: the
+  // over-read rows are L2 hits that warm the next chunk, profiles/r05w_flow_prefetch_ab.txt), so
+  // there they are still loaded.
   auto prefetch = [&](uint32_t k) -> u32x4 {
-    return k < steps ? flow_load_x(a, in_rec, base, k, rem) : u32x4{0u, 0u, 0u, 0u};
+    return (!OWN || k < steps) ? flow_load_x(a, in_rec, base, k, rem) : u32x4{0u, 0u, 0u, 0u};
   };
   CtrCache cc;
   uint32_t cc_win = 0xffffffffu;
@@ -696,7 +700,9 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
   return pw;
 }
 
-template <bool DECRYPT, int NT, bool DK>
+// HOSTIN: the records are in host memory (device addresses of page-locked pages): each unit reads
+// only its own input rows (flow_unit<.., OWN>).
+template <bool DECRYPT, int NT, bool DK, bool HOSTIN = false>
 __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
   CMPI_PROBE(a, 0u);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -713,7 +719,7 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
       uint32_t r, i, steps;
       const int32_t base = flow_unit_base(a, u, r, i, steps);
       va0 = flow_load_x(a, a.in + (uint64_t)r * a.in_stride, base, 0u, rem);
-      if (steps > 1u) vb0 = flow_load_x(a, a.in + (uint64_t)r * a.in_stride, base, 1u, rem);
+      if (!HOSTIN || steps > 1u) vb0 = flow_load_x(a, a.in + (uint64_t)r * a.in_stride, base, 1u, rem);
     }
   }
   stage_flow<NT>(a);
@@ -727,7 +733,7 @@ __global__ __launch_bounds__(NT) void gcm_flow_kernel(GcmArgs a) {
     u32x4 pw = {0u, 0u, 0u, 0u};
     uint32_t r = 0xffffffffu;
     if (u < units)  // wave-uniform
-      pw = flow_unit<DECRYPT, DK>(a, rk, rl, lenblk, u, ub == blockIdx.x * wpb, va0, vb0, r);
+      pw = flow_unit<DECRYPT, DK, false, HOSTIN>(a, rk, rl, lenblk, u, ub == blockIdx.x * wpb, va0, vb0, r);
     if (DK || !a.one_wg) {  // partials for the combine launch, stored write-through like the records
       if (u < units && lane == 0u) st_wt(wt_rsrc(reinterpret_cast<const uint8_t*>(a.partial)), 16u * u, pw);
       continue;

@@ -233,11 +233,19 @@ int svc_stop_locked(Svc& S) {
   return CMPI_OK;
 }
 
-// Stop and free the context's service (hmu held).
+// Stop and free the context's service (hmu held).  If the stop failed (its launch event could not
+// be waited), the generation may still be resident: its memory is freed only once its exit word
+// shows it left (200 ms bound); otherwise it is left allocated — a leak, never a
+// kernel polling or writing freed memory.
 int svc_shutdown_locked(cmpi_ctx* c) {
   if (!c->svc) return CMPI_OK;
-  const int rc = svc_stop_locked(*c->svc);
-  svc_release(*c->svc);
+  Svc& S = *c->svc;
+  const int rc = svc_stop_locked(S);
+  bool gone = !rc || !S.launched || svc_exited(S);
+  for (const auto t0 = std::chrono::steady_clock::now();
+       !gone && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200);)
+    gone = svc_exited(S);
+  if (gone) svc_release(S);
   delete c->svc;
   c->svc = nullptr;
   return rc;

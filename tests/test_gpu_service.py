@@ -170,7 +170,45 @@ def test_service_many_contexts_share_slots():
     for c in ctxs:
         c.service_stop()
         c.close()
-    assert max(lat[6:]) < 0.005, [round(v * 1e3, 2) for v in lat]
+    # the failure this guards against waited for a resident kernel's idle-out / lifetime (>= 100 ms
+    # here): 50 ms leaves a loaded box its margin
+    assert max(lat[6:]) < 0.05, [round(v * 1e3, 2) for v in lat]
+
+
+def test_service_many_contexts_two_threads():
+    """Two host threads, each round-robin over three of six serviced contexts (4 stream slots):
+    launches on held slots kick other threads' generations while their messages are posted; every
+    message completes bit-exact (the concurrent kick / relaunch path)."""
+    import threading
+
+    keys = [bytes([k + 31] * 16) for k in range(6)]
+    ctxs = [aead.AeadCtx(k) for k in keys]
+    for c in ctxs:
+        c.service_start(500000)
+    errors = []
+
+    def worker(t):
+        try:
+            for i in range(30):
+                k = 3 * t + i % 3
+                pt = splitmix64_bytes(1000 * t + i, 700 + 37 * i).tobytes()
+                nonce = splitmix64_bytes(5000 * t + i, 12).tobytes()
+                got = ctxs[k].seal(nonce, pt)
+                if got != oracle.gcm_seal(keys[k], nonce, pt) or ctxs[k].open(nonce, got) != pt:
+                    errors.append((t, i))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=60)
+    for c in ctxs:
+        c.service_stop()
+        c.close()
+    assert not any(x.is_alive() for x in th)
+    assert errors == []
 
 
 def test_service_leaves_other_streams_free():
@@ -199,7 +237,7 @@ def test_service_leaves_other_streams_free():
     assert ctx.service_running()  # still resident: nothing above waited for it to exit
     ctx.service_stop()
     ctx.close()
-    assert max(lat) < 0.02, [round(v * 1e3, 2) for v in lat]
+    assert max(lat) < 0.05, [round(v * 1e3, 2) for v in lat]  # was: up to the kernel's 100 ms lifetime
 
 
 def test_service_refuses_other_contexts():

@@ -14,6 +14,8 @@
 #include <string>
 #include <vector>
 
+#include <sched.h>
+
 #include "../include/cmpi_aead.h"
 #include "../include/cmpi_debug.h"
 #include "../include/cmpi_ctrmode.h"
@@ -54,6 +56,45 @@ __global__ void busy_kernel(unsigned us, unsigned* flag, unsigned seq) {
   if (flag && threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Bind this process to the CPUs of the GPU's NUMA node that it may run on (as
+// an MPI launcher's --bind-to numa does), before any page-locked allocation (first touch): from
+// the far socket every served message pays ≈ 0.9 µs more per PCIe round trip (DESIGN.md §5 "Host
+// NUMA placement").  CMPI_NUMA_BIND=0 keeps the inherited placement.  Returns the GPU's node
+// (-1 unknown) and sets *bound to the number of CPUs bound (0: not bound).
+static int bind_gpu_node(int dev, int* bound) {
+  *bound = 0;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) return -1;
+  for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
+  char path[160];
+  snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE* f = fopen(path, "r");
+  int node = -1;
+  if (!f) return -1;
+  if (fscanf(f, "%d", &node) != 1) node = -1;
+  fclose(f);
+  const char* env = getenv("CMPI_NUMA_BIND");
+  if (node < 0 || (env && atoi(env) == 0)) return node;
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  if (!(f = fopen(path, "r"))) return node;
+  char list[4096] = {0};
+  const bool ok = fgets(list, sizeof list, f) != nullptr;
+  fclose(f);
+  if (!ok) return node;
+  cpu_set_t allowed, want;
+  CPU_ZERO(&want);
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return node;
+  for (char* tok = strtok(list, ",\n"); tok; tok = strtok(nullptr, ",\n")) {  // "a-b,c,..."
+    int a = -1, b = -1;
+    if (sscanf(tok, "%d-%d", &a, &b) < 2) b = a;
+    for (int c = a; c >= 0 && c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &allowed)) CPU_SET(c, &want);
+  }
+  const int n = CPU_COUNT(&want);
+  if (n > 0 && sched_setaffinity(0, sizeof want, &want) == 0) *bound = n;
+  return node;
+}
+
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -80,6 +121,8 @@ static void spin(hipStream_t s) {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 2000;
+  int numa_cpus = 0;
+  const int numa_node = bind_gpu_node(0, &numa_cpus);
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   std::string js = "{";
@@ -88,6 +131,8 @@ int main(int argc, char** argv) {
     snprintf(b, sizeof b, "%s\"%s\": %.2f", js.size() > 1 ? ", " : "", k, v);
     js += b;
   };
+  put("numa_gpu_node", numa_node);
+  put("numa_bound_cpus", numa_cpus);  // 0: the inherited placement (not bound)
   put("empty_launch_sync_us", median_us(iters, [&] {
         empty_kernel<<<1, 64, 0, s>>>();
         CK(hipStreamSynchronize(s));

@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=r05w
+timeout -k 10 420 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/${R}_gpu_tests.log 2>&1 || exit $?
+timeout -k 10 150 tools/msg_latency 2000 > gpurun_out/${R}_msg_latency.json 2> gpurun_out/${R}_msg_latency.err || exit $?
+timeout -k 10 300 python tools/flow_ab.py ab/base/libcmpi_aead.so ab/pf/libcmpi_aead.so 3 > gpurun_out/${R}_flow_prefetch_ab.txt 2>&1 || exit $?
+timeout -k 10 200 python tools/sustained_ab.py ab/base/libcmpi_aead.so ab/pf/libcmpi_aead.so 3 alltoall > gpurun_out/${R}_alltoall_prefetch_ab.txt 2>&1 || exit $?
+timeout -k 10 120 python tools/svc_timeline.py > gpurun_out/${R}_svc_timeline.jsonl 2> gpurun_out/${R}_svc_timeline.err || exit $?
+echo DONE
