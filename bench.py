@@ -631,7 +631,7 @@ def _peer_send(dev, rank: int, nblk: int, n: int):
     return torch.randint(0, 256, (nblk * n,), dtype=torch.uint8, device=dev, generator=g)
 
 
-def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, warmup: int = 3) -> dict:
+def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 100, warmup: int = 10) -> dict:
     """BASELINE config 5 end to end, MPIR_Naive_Sec_Alltoall (alltoall.c:764-836) per rank:
     seal the rank's 8 peer blocks (config 5's p = 8) with fresh nonces into the wire layout
     nonce||ct||tag (one batched call), exchange the wire blocks, open the 8 received blocks (one
