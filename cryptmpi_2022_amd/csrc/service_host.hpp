@@ -69,8 +69,8 @@ uint32_t svc_groups(uint32_t op, size_t len, uint32_t ls_min) {
   if (op != cmpi::dev::kSvcSeal && op != cmpi::dev::kSvcOpen) return 1;
   const uint32_t nx = (uint32_t)((len + 15) >> 4);
   uint32_t ls = ls_min;
-  while (ls < 3u && nx >= (cmpi::dev::kSvcMaxChunks + 1u) * (64u << ls)) ++ls;
-  const uint32_t C = 64u << ls, nch = nx >= C ? nx / C : 1u;
+  while (ls < 3u && nx > cmpi::dev::kSvcMaxChunks * (64u << ls)) ++ls;
+  const uint32_t C = 64u << ls, nch = nx ? (nx + C - 1u) / C : 1u;
   return (nch + cmpi::dev::kSvcChunkWaves - 1u) / cmpi::dev::kSvcChunkWaves;
 }
 

@@ -51,10 +51,18 @@
 namespace cmpi {
 namespace dev {
 
-constexpr uint32_t kSvcChunkWaves = 8u;  // chunk waves per workgroup
-constexpr uint32_t kSvcThreads = 576u;   // + the J0 wave (svc_j0_wave; idle in workgroups > 0)
-constexpr uint32_t kSvcGroups = 8u;      // workgroups (one per XCD when the chip is free)
-constexpr uint32_t kSvcMaxChunks = 64u;  // kSvcGroups x kSvcChunkWaves
+// Workgroups of the resident grid (8 = one per XCD when the chip is free, 8 CUs held while
+// resident).  16 workgroups of 4 chunk waves (-DCMPI_SVC_GROUPS=16) served 64 KiB seal / open
+// 0.5-1 us faster and 1 KiB 0.4 us faster on the same box, pageable 64 KiB 1 us slower
+// (profiles/r05ac_*), at 16 CUs held between messages: not the default.
+#ifndef CMPI_SVC_GROUPS
+#define CMPI_SVC_GROUPS 8
+#endif
+constexpr uint32_t kSvcGroups = CMPI_SVC_GROUPS;         // workgroups (8: one per XCD when the chip is free)
+constexpr uint32_t kSvcMaxChunks = 64u;                  // kSvcGroups x kSvcChunkWaves
+constexpr uint32_t kSvcChunkWaves = kSvcMaxChunks / kSvcGroups;  // chunk waves per workgroup
+constexpr uint32_t kSvcThreads = 64u * (kSvcChunkWaves + 1u);    // + the J0 wave (svc_j0_wave; idle in workgroups > 0)
+constexpr uint32_t kSvcStage = kSvcChunkWaves >= 8u ? 512u : 256u;  // threads that stage the tables
 constexpr uint32_t kSvcSeal = 0u, kSvcOpen = 1u, kSvcStop = 2u, kSvcXor = 3u, kSvcCtr = 4u, kSvcEcb = 5u;
 // descriptor words: op, len, in lo/hi, out lo/hi, then the op's own: GCM nonce[3] at 6..8, XOR
 // mask lo/hi at 6..7, CTR counter block as big-endian halves hi lo/hi, lo lo/hi at 8..11
@@ -161,14 +169,17 @@ __device__ __forceinline__ uint64_t lds_ptr64(uint32_t off) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Chunk plan of a message of `len` bytes: C = 64·2^ls data blocks per chunk, nch chunks (chunk 0
-// takes the remainder), ngrp workgroups of 8 chunks.
+// Chunk plan of a message of `len` bytes: C = 64·2^ls data blocks per chunk (the smallest of at
+// most 64 chunks), nch = ceil(blocks / C) chunks, chunk 0 taking the remainder (1..C blocks), so
+// no chunk runs more than S = C/64 steps (round 5: chunk 0 took C..2C-1 blocks, two steps for
+// e.g. 65 000 B where one suffices); ngrp workgroups of kSvcChunkWaves chunks.  service_host.hpp
+// svc_groups mirrors it.
 __device__ __forceinline__ uint32_t svc_plan(uint32_t len, uint32_t& ls, uint32_t& nch, uint32_t ls_min = 0u) {
   const uint32_t nx = (len + 15u) >> 4;
   ls = ls_min;
-  while (ls < 3u && nx >= (kSvcMaxChunks + 1u) * (64u << ls)) ++ls;
+  while (ls < 3u && nx > kSvcMaxChunks * (64u << ls)) ++ls;
   const uint32_t C = 64u << ls;
-  nch = nx >= C ? nx / C : 1u;
+  nch = nx ? (nx + C - 1u) / C : 1u;
   return (nch + kSvcChunkWaves - 1u) / kSvcChunkWaves;
 }
 
@@ -198,7 +209,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   a.nfix[1] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 36u));
   a.nfix[2] = __builtin_amdgcn_readfirstlane(lds32(kSvcX + 40u));
   const uint32_t nx = a.nb;  // data blocks (the X-sequence less its length block)
-  uint32_t ls, nch;  // chunk 0: C <= r0 < 2C (or the whole message)
+  uint32_t ls, nch;  // chunk 0: 1 <= r0 <= C blocks (0 for an empty message)
   const uint32_t ngrp = svc_plan(len, ls, nch, s.ls_min);  // workgroups with chunks
   const uint32_t C = 64u << ls;
   a.S = 1u << ls;
@@ -212,7 +223,7 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   const uint64_t cbits = (uint64_t)len * 8u;
   const u32x4 lenblk = {0u, 0u, __builtin_bswap32((uint32_t)(cbits >> 32)), __builtin_bswap32((uint32_t)cbits)};
   const uint32_t u = wg * wpb + wv;
-  if (threadIdx.x == 0u) SVC_STAMP(s, seq, 2u + wg);
+  if (threadIdx.x == 0u && wg < 8u) SVC_STAMP(s, seq, 2u + wg);  // (stamps of workgroups 0..7)
   u32x4 pw = {0u, 0u, 0u, 0u};
   if (wv == wpb) {  // the J0 wave (workgroup 0's)
     if (wg == 0u) pw = svc_j0_wave(a, s.rk, rl, lenblk);
@@ -224,12 +235,12 @@ __device__ __forceinline__ void svc_message(const SvcArgs& s, const RowLanes& rl
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores are performed
   __syncthreads();
   if (threadIdx.x == 0u) {
-    SVC_STAMP(s, seq, 10u + wg);
+    if (wg < 8u) SVC_STAMP(s, seq, 10u + wg);
     u32x4 x = lds128(kFlowAgg);
     for (uint32_t j = 1; j <= wpb; ++j) x ^= lds128(kFlowAgg + 16u * j);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's record bytes reach the host first
     svc_post(s.done + 8u * wg, seq, x);
-    SVC_STAMP(s, seq, 18u + wg);
+    if (wg < 8u) SVC_STAMP(s, seq, 18u + wg);
   }
 }
 
@@ -298,7 +309,7 @@ __global__ __launch_bounds__(kSvcThreads) void gcm_service_kernel(SvcArgs s) {
     GcmArgs t{};
     t.te0 = s.te0;
     t.wtab = s.wtab;
-    if (threadIdx.x < 512u) stage_flow_tables<512>(t);
+    if (threadIdx.x < kSvcStage) stage_flow_tables<kSvcStage>(t);
     __syncthreads();
   } else {  // CTR / ECB contexts: the AES rows only
     stage_rows(s.te0, kGcmRows);

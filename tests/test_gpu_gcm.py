@@ -436,7 +436,8 @@ def test_config2_full_batch_properties(n):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("n,nrec", [(0, 1), (1, 1), (777, 20), (65536, 1), (1 << 20, 1), (100000, 3)])
+@pytest.mark.parametrize("n,nrec", [(0, 1), (1, 1), (777, 20), (65536, 1), (1 << 20, 1), (100000, 3),
+                                    ((1 << 20) + 5, 2), ((8 << 20) - 3, 1)])
 @pytest.mark.parametrize("pinned", [False, True])
 def test_host_direct_single_messages(n, nrec, pinned):
     """Single MPI messages through cmpi_gcm_seal_host / open_host (the EVP drop-in's and the 600

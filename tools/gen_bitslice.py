@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generator of cryptmpi_2022_amd/csrc/aes_bitslice_gen.hpp: bitsliced AES-128 rounds for gfx950
+"""Generator of tools/probe/aes_bitslice_gen.hpp (git-ignored; tools/probe/bitslice_probe.hip): bitsliced AES-128 rounds for gfx950
 as v_bitop3_b32 (3-input LUT) networks.
 
 Bitsliced layout (csrc/aes_bitslice.hpp): a lane's 32-bit register holds ONE bit of the state
@@ -535,13 +535,12 @@ def bop1(args, tt):
 def main():
     gates = parse_bp()
     check_bp(gates)
-    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cryptmpi_2022_amd", "csrc",
-                            "aes_bitslice_gen.hpp")
+    out_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "probe", "aes_bitslice_gen.hpp")
     parts = ["// aes_bitslice_gen.hpp — GENERATED by tools/gen_bitslice.py; do not edit.\n"
-             "// Bitsliced AES-128 rounds as gfx950 v_bitop3_b32 networks (see csrc/aes_bitslice.hpp).\n"
+             "// Bitsliced AES-128 rounds as gfx950 v_bitop3_b32 networks (tools/probe/bitslice_probe.hip).\n"
              "#pragma once\n#include <stdint.h>\n\nnamespace cmpi::bs {\n\n"
-             "__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c, int tt) {\n"
-             "  return __builtin_amdgcn_bitop3_b32(a, b, c, tt);\n}\n"]
+             "// the truth table must be a compile-time constant of the builtin: a macro, not a function\n"
+             "#define bop3(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))\n\n"]
     for last in (False, True):
         g, ins, keys, outs = build_round(last)
         luts, best = map_lut3(g, outs)
@@ -551,7 +550,7 @@ def main():
               f"(3-in {sizes.count(3)}, 2-in {sizes.count(2)}, 1-in {sizes.count(1)}), "
               f"{len(luts) / 32:.1f} per block", file=sys.stderr)
         parts.append("\n" + emit(g, luts, best, ins, keys, outs, last, "round_last" if last else "round_mid"))
-    parts.append("\n}  // namespace cmpi::bs\n")
+    parts.append("\n}  // namespace cmpi::bs\n#undef bop3\n")
     if "--dry" not in sys.argv:
         with open(out_path, "w") as f:
             f.write("".join(parts))
