@@ -1202,6 +1202,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   return CMPI_OK;
 }
 
+std::atomic<int> g_ctr_wg_per_cu{2};  // cmpi_debug_set_ctr_wg_per_cu (co-residence experiments)
+
 int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, const uint8_t ctr[16],
                       void* stream) {
   if (!c) return fail(CMPI_EINVAL, "null ctx");
@@ -1222,7 +1224,8 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   a.rk = folded(c->rk);
   a.sched = kSched;
   const uint64_t blocks = (a.nblk + 1023) / 1024;
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * 2));
+  const uint32_t grid =
+      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * (uint64_t)g_ctr_wg_per_cu.load()));
   hipStream_t st = (hipStream_t)stream;
   auto fn = in ? cmpi::dev::ctr_kernel<true> : cmpi::dev::ctr_kernel<false>;
   const int lds = 65536;
@@ -1449,6 +1452,7 @@ void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }
 void cmpi_debug_set_svc_ls_min(int ls) { g_svc_ls_min.store(ls >= 0 && ls <= 3 ? ls : 0); }
 void cmpi_debug_set_lane_pair(int on) { g_lane_pair.store(on >= 1 && on <= 4 ? on : 0); }
 void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 || threads == 1024 ? threads : 0); }
+void cmpi_debug_set_ctr_wg_per_cu(int n) { g_ctr_wg_per_cu.store(n >= 1 && n <= 2 ? n : 2); }
 
 // Timing events without the system-scope release fence (hipEventDisableSystemFence): a default
 // event's fence writes back and invalidates the caches and leaves a ~6 us bubble before the

@@ -41,6 +41,9 @@ void cmpi_debug_event_free(void* ev);
 /* gcm_flow_kernel threads per workgroup: 0 automatic (always 512 since round 4: the 1024-thread
  * form spills), 512 or 1024 forced (the chunk plan then assumes that many waves per CU). */
 void cmpi_debug_set_flow_threads(int threads);
+/* ctr_kernel workgroups per CU (1 or 2; default 2 = every VGPR of the CU): 1 leaves room for a
+ * co-resident kernel (tools/probe/hybrid_ctr_probe.hip). */
+void cmpi_debug_set_ctr_wg_per_cu(int n);
 /* gcm_lane_kernel (L = 4) record stores grouped by 128-byte output line (each line stored whole in
  * the step that completes it), on batches of at least one group per thread of the grid: 2 =
  * predicated selects (default), 1 = branches, 0 = a store per step; 3 / 4 = the select / branch
