@@ -8,6 +8,7 @@
 // Each thread owns two 16-byte blocks per iteration (ILP for the LDS pipe), consecutive lanes
 // own consecutive blocks (1 KiB coalesced per wave-instruction).
 #pragma once
+#include "aes_bitslice_gen.hpp"
 #include "aes_device.hpp"
 
 namespace cmpi {
@@ -148,6 +149,75 @@ __global__ __launch_bounds__(256) void xor_bytes_kernel(uint8_t* out, const uint
   }
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n - 16u * nv) out[16u * nv + t] = a[16u * nv + t] ^ b[16u * nv + t];
+}
+
+// ---------------------------------------------------------------- bitsliced CTR (VALU AES)
+// The T-table kernels above are bound by the LDS array; this one runs AES on the VALU as a
+// bitsliced network (aes_bitslice_gen.hpp, tools/gen_bitslice.py: v_bitop3 LUTs, 32 blocks per
+// lane, no LDS), so the two can share the CUs: cmpi_ctr_xor hands a fraction of a long stream to
+// it on a second stream while ctr_kernel runs the rest at one workgroup per CU
+// (profiles/r05ae_hybrid_ctr_probe.jsonl: 1 444 -> 1 572 GiB/s on 1 GiB).
+// A wave's chunk is 2 048 blocks; lane L holds blocks c + L + 64 j (j < 32), so load / store j
+// of the wave touches 1 KiB of contiguous stream.  Planes: plane p = bit (p % 8) of state byte
+// p / 8, bit j of a plane = block j; key planes (DevTables::bsk) are 0 / ~0: round 0 and 10 the
+// round keys, rounds 1-9 InvMixColumns of them (the network adds the key before MixColumns).
+struct CtrBsArgs {  // + in (null: keystream only), out, kp (11 x 128 key planes) as kernel parameters
+  uint64_t nchunks;   // 2 048-block chunks, from block 0 of (in, out)
+  uint64_t ctr_hi, ctr_lo;
+};
+
+// In-place 32 x 32 bit transpose: on exit x[r] bit c = (x[c] bit r on entry).
+__device__ __forceinline__ void bs_transpose32(uint32_t* x) {
+  uint32_t m = 0x0000ffffu;
+#pragma unroll
+  for (int j = 16; j != 0; j >>= 1, m ^= m << j) {
+#pragma unroll
+    for (int k = 0; k < 32; k = (k + j + 1) & ~j) {
+      const uint32_t t = ((x[k] >> j) ^ x[k + j]) & m;
+      x[k] ^= t << j;
+      x[k + j] ^= t;
+    }
+  }
+}
+
+// (in, out, kp as restrict parameters: the key planes then load as scalars — read through the
+// argument struct they took VGPRs, 101 AGPRs of spill and one wave per SIMD.  Bounded to 256
+// registers (2 waves per SIMD alone, one beside ctr_kernel's four): the counter / keystream
+// transposes before and after the rounds spill ~70 registers to scratch.)
+__global__ __launch_bounds__(256, 2) void ctr_bs_kernel(CtrBsArgs a, const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                     const uint32_t* __restrict__ kp) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6, nwaves = (uint64_t)gridDim.x * 4u;
+  for (uint64_t ch = wave; ch < a.nchunks; ch += nwaves) {  // wave-uniform
+    const uint64_t b0 = ch * 2048u + lane;
+    uint32_t s[128];
+    // counter blocks -> planes: s[32 w + j] = word w of block j, transposed to s[32 w + r] = plane
+    // 32 w + r (bit r of word w = bit r % 8 of state byte 4 w + r / 8)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        uint32_t w0, w1, w2, w3;
+        ctr_words(a.ctr_hi, a.ctr_lo, b0 + 64u * (uint64_t)j, w0, w1, w2, w3);
+        s[32 * w + j] = w == 0 ? w0 : w == 1 ? w1 : w == 2 ? w2 : w3;
+      }
+      bs_transpose32(s + 32 * w);
+    }
+#pragma unroll
+    for (int p = 0; p < 128; ++p) s[p] ^= kp[p];
+#pragma unroll 1
+    for (int r = 1; r < 10; ++r) bs::round_mid(s, kp + 128 * r);
+    bs::round_last(s, kp + 128 * 10);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) bs_transpose32(s + 32 * w);  // s[32 w + j] = word w of block j's keystream
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const uint64_t b = b0 + 64u * (uint64_t)j;
+      u32x4 v = {s[j], s[32 + j], s[64 + j], s[96 + j]};
+      if (in) v ^= in[b];
+      out[b] = v;
+    }
+  }
 }
 
 // Streaming device copy (the measured HBM peak of bench.py's roofline, cmpi_debug_copy): 16 B

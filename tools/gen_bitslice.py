@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generator of tools/probe/aes_bitslice_gen.hpp (git-ignored; tools/probe/bitslice_probe.hip): bitsliced AES-128 rounds for gfx950
+"""Generator of cryptmpi_2022_amd/csrc/aes_bitslice_gen.hpp (ctr_kernels.hpp ctr_bs_kernel, tools/probe/*): bitsliced AES-128 rounds for gfx950
 as v_bitop3_b32 (3-input LUT) networks.
 
 Bitsliced layout (csrc/aes_bitslice.hpp): a lane's 32-bit register holds ONE bit of the state
@@ -535,9 +535,10 @@ def bop1(args, tt):
 def main():
     gates = parse_bp()
     check_bp(gates)
-    out_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "probe", "aes_bitslice_gen.hpp")
+    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cryptmpi_2022_amd", "csrc",
+                            "aes_bitslice_gen.hpp")
     parts = ["// aes_bitslice_gen.hpp — GENERATED by tools/gen_bitslice.py; do not edit.\n"
-             "// Bitsliced AES-128 rounds as gfx950 v_bitop3_b32 networks (tools/probe/bitslice_probe.hip).\n"
+             "// Bitsliced AES-128 rounds as gfx950 v_bitop3_b32 networks (ctr_kernels.hpp ctr_bs_kernel).\n"
              "#pragma once\n#include <stdint.h>\n\nnamespace cmpi::bs {\n\n"
              "// the truth table must be a compile-time constant of the builtin: a macro, not a function\n"
              "#define bop3(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))\n\n"]
