@@ -185,37 +185,60 @@ __device__ __forceinline__ void bs_transpose32(uint32_t* x) {
 // registers (2 waves per SIMD alone, one beside ctr_kernel's four): the counter / keystream
 // transposes before and after the rounds spill ~70 registers to scratch.)
 __global__ __launch_bounds__(256, 2) void ctr_bs_kernel(CtrBsArgs a, const u32x4* __restrict__ in, u32x4* __restrict__ out,
-                                                     const uint32_t* __restrict__ kp) {
+                                                        const uint32_t* __restrict__ kp) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6, nwaves = (uint64_t)gridDim.x * 4u;
+  const uint32_t* __restrict__ in32 = reinterpret_cast<const uint32_t*>(in);
+  uint32_t* __restrict__ out32 = reinterpret_cast<uint32_t*>(out);
   for (uint64_t ch = wave; ch < a.nchunks; ch += nwaves) {  // wave-uniform
     const uint64_t b0 = ch * 2048u + lane;
     uint32_t s[128];
-    // counter blocks -> planes: s[32 w + j] = word w of block j, transposed to s[32 w + r] = plane
-    // 32 w + r (bit r of word w = bit r % 8 of state byte 4 w + r / 8)
+    // counter blocks -> planes (plane 32 w + r = bit r of word w = bit r % 8 of state byte
+    // 4 w + r / 8; bit j of a plane = block j).  When no 32-bit carry falls inside the chunk
+    // (all but one chunk in 2^21), words 0-2 are the chunk's own constants — their planes are
+    // 0 / ~0 — and only word 3 is transposed (fewer live registers than four transposes)
+    const uint64_t c_lo = a.ctr_lo + ch * 2048u;  // the chunk's first counter (low half)
+    const uint64_t c_hi = a.ctr_hi + (c_lo < a.ctr_lo ? 1u : 0u);
+    if ((uint32_t)c_lo <= 0xffffffffu - 2047u) {
+      const uint32_t w0 = __builtin_bswap32((uint32_t)(c_hi >> 32)), w1 = __builtin_bswap32((uint32_t)c_hi),
+                     w2 = __builtin_bswap32((uint32_t)(c_lo >> 32));
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        uint32_t w0, w1, w2, w3;
-        ctr_words(a.ctr_hi, a.ctr_lo, b0 + 64u * (uint64_t)j, w0, w1, w2, w3);
-        s[32 * w + j] = w == 0 ? w0 : w == 1 ? w1 : w == 2 ? w2 : w3;
+      for (int r = 0; r < 32; ++r) {
+        s[r] = (w0 >> r) & 1u ? 0xffffffffu : 0u;
+        s[32 + r] = (w1 >> r) & 1u ? 0xffffffffu : 0u;
+        s[64 + r] = (w2 >> r) & 1u ? 0xffffffffu : 0u;
       }
-      bs_transpose32(s + 32 * w);
+      const uint32_t l0 = (uint32_t)c_lo + lane;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) s[96 + j] = __builtin_bswap32(l0 + 64u * (uint32_t)j);
+      bs_transpose32(s + 96);
+    } else {  // a 32-bit carry inside the chunk: every word per block
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          uint32_t w0, w1, w2, w3;
+          ctr_words(a.ctr_hi, a.ctr_lo, b0 + 64u * (uint64_t)j, w0, w1, w2, w3);
+          s[32 * w + j] = w == 0 ? w0 : w == 1 ? w1 : w == 2 ? w2 : w3;
+        }
+        bs_transpose32(s + 32 * w);
+      }
     }
 #pragma unroll
     for (int p = 0; p < 128; ++p) s[p] ^= kp[p];
 #pragma unroll 1
     for (int r = 1; r < 10; ++r) bs::round_mid(s, kp + 128 * r);
     bs::round_last(s, kp + 128 * 10);
+    // keystream out one word at a time: transpose group w (s[32 w + j] = word w of block j), XOR
+    // word w of each block, store it — a group's registers are free before the next is transposed
 #pragma unroll
-    for (int w = 0; w < 4; ++w) bs_transpose32(s + 32 * w);  // s[32 w + j] = word w of block j's keystream
+    for (int w = 0; w < 4; ++w) {
+      bs_transpose32(s + 32 * w);
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const uint64_t b = b0 + 64u * (uint64_t)j;
-      u32x4 v = {s[j], s[32 + j], s[64 + j], s[96 + j]};
-      if (in) v ^= in[b];
-      out[b] = v;
+      for (int j = 0; j < 32; ++j) {
+        const uint64_t i = 4u * (b0 + 64u * (uint64_t)j) + (uint64_t)w;
+        out32[i] = in32 ? in32[i] ^ s[32 * w + j] : s[32 * w + j];
+      }
     }
   }
 }
