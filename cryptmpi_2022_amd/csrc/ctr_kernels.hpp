@@ -188,8 +188,6 @@ __global__ __launch_bounds__(256, 2) void ctr_bs_kernel(CtrBsArgs a, const u32x4
                                                         const uint32_t* __restrict__ kp) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6, nwaves = (uint64_t)gridDim.x * 4u;
-  const uint32_t* __restrict__ in32 = reinterpret_cast<const uint32_t*>(in);
-  uint32_t* __restrict__ out32 = reinterpret_cast<uint32_t*>(out);
   for (uint64_t ch = wave; ch < a.nchunks; ch += nwaves) {  // wave-uniform
     const uint64_t b0 = ch * 2048u + lane;
     uint32_t s[128];
@@ -229,16 +227,24 @@ __global__ __launch_bounds__(256, 2) void ctr_bs_kernel(CtrBsArgs a, const u32x4
 #pragma unroll 1
     for (int r = 1; r < 10; ++r) bs::round_mid(s, kp + 128 * r);
     bs::round_last(s, kp + 128 * 10);
-    // keystream out one word at a time: transpose group w (s[32 w + j] = word w of block j), XOR
-    // word w of each block, store it — a group's registers are free before the next is transposed
+    // keystream out: s[32 w + j] = word w of block j's keystream after the four transposes; the
+    // blocks leave as 16-byte XORs in four batches of 8 (the compiler barrier keeps a batch's loads
+    // from being hoisted over the previous batch's stores: all 32 in flight took 128 more
+    // registers and spilled, two batches of 16 still spilled 17)
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      bs_transpose32(s + 32 * w);
+    for (int w = 0; w < 4; ++w) bs_transpose32(s + 32 * w);
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const uint64_t i = 4u * (b0 + 64u * (uint64_t)j) + (uint64_t)w;
-        out32[i] = in32 ? in32[i] ^ s[32 * w + j] : s[32 * w + j];
+    for (int h = 0; h < 4; ++h) {
+      u32x4 v[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = 8 * h + jj;
+        v[jj] = u32x4{s[j], s[32 + j], s[64 + j], s[96 + j]};
+        if (in) v[jj] ^= in[b0 + 64u * (uint64_t)j];
       }
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) out[b0 + 64u * (uint64_t)(8 * h + jj)] = v[jj];
+      asm volatile("" ::: "memory");
     }
   }
 }
