@@ -1214,8 +1214,8 @@ std::atomic<int> g_ctr_wg_per_cu{2};  // cmpi_debug_set_ctr_wg_per_cu (co-reside
 // Long CTR streams: this share (per mille) of the whole 2 048-block chunks goes to the bitsliced
 // kernel (VALU) on the context's second stream while ctr_kernel (LDS) runs the rest at one
 // workgroup per CU; streams from g_ctr_hybrid_min bytes (cmpi_debug_set_ctr_hybrid).  Off by
-// default: the timing probe ran 1 572 vs 1 444 GiB/s at 15 % (r05ae), the product kernel — which
-// spills ~70 registers around its transposes — 1 426 vs 1 453 (r05af_ctr_hybrid_sweep.jsonl).
+// default: the timing probe ran 1 572 vs 1 444 GiB/s at 15 % (r05ae), the product kernel — spill-
+// free, 715 GiB/s alone — 1 399 vs 1 392-1 397, parity (r05am_ctr_hybrid_sweep.jsonl).
 std::atomic<uint64_t> g_ctr_hybrid_min{(uint64_t)64 << 20};
 std::atomic<int> g_ctr_hybrid_permille{0};
 
@@ -1241,7 +1241,12 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   int wg_per_cu = g_ctr_wg_per_cu.load();
   // the bitsliced share: whole 2 048-block chunks from the stream's start
   const int pm = g_ctr_hybrid_permille.load();
-  const uint64_t bs_chunks = n >= g_ctr_hybrid_min.load() && pm > 0 ? (n / 16) * (uint64_t)pm / 1000u / 2048u : 0;
+  uint64_t bs_chunks = n >= g_ctr_hybrid_min.load() && pm > 0 ? (n / 16) * (uint64_t)pm / 1000u / 2048u : 0;
+  {  // the bitsliced kernel takes no chunk with a 32-bit counter carry inside: stop before the first
+    const uint64_t lo = cmpi::be64(ctr + 8);
+    const uint64_t to_carry = (0x100000000ull - (lo & 0xffffffffull)) / 2048u;  // whole chunks before it
+    if (bs_chunks > to_carry) bs_chunks = to_carry;
+  }
   std::unique_lock<std::mutex> bs_lk(c->bs_mu, std::defer_lock);
   if (bs_chunks) {
     bs_lk.lock();  // this call's fork / join on the context's second stream
@@ -1254,9 +1259,12 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
     b.nchunks = bs_chunks;
     b.ctr_hi = a.ctr_hi;
     b.ctr_lo = a.ctr_lo;
-    HIP_TRY(launch_k(cmpi::dev::ctr_bs_kernel, dim3((uint32_t)std::min<uint64_t>(bs_chunks, (uint64_t)c->ncu)), dim3(256), 0,
-                     c->bs_st, b, reinterpret_cast<const u32x4*>(in), reinterpret_cast<u32x4*>(out),
-                     static_cast<const uint32_t*>(c->dt->bsk[0])));
+    const dim3 bsg((uint32_t)std::min<uint64_t>(bs_chunks, (uint64_t)c->ncu));
+    const u32x4* bin = reinterpret_cast<const u32x4*>(in);
+    u32x4* bout = reinterpret_cast<u32x4*>(out);
+    const uint32_t* bkp = c->dt->bsk[0];
+    HIP_TRY(in ? launch_k(cmpi::dev::ctr_bs_kernel<true>, bsg, dim3(256), 0, c->bs_st, b, bin, bout, bkp)
+               : launch_k(cmpi::dev::ctr_bs_kernel<false>, bsg, dim3(256), 0, c->bs_st, b, bin, bout, bkp));
     const uint64_t skip = bs_chunks * 2048u, sb = skip * 16u;  // the T-table kernel takes the rest
     a.in = in ? in + sb : nullptr;
     a.out = out + sb;

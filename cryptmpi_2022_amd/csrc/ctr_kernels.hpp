@@ -184,6 +184,7 @@ __device__ __forceinline__ void bs_transpose32(uint32_t* x) {
 // argument struct they took VGPRs, 101 AGPRs of spill and one wave per SIMD.  Bounded to 256
 // registers (2 waves per SIMD alone, one beside ctr_kernel's four): the counter / keystream
 // transposes before and after the rounds spill ~70 registers to scratch.)
+template <bool XOR_IN>
 __global__ __launch_bounds__(256, 2) void ctr_bs_kernel(CtrBsArgs a, const u32x4* __restrict__ in, u32x4* __restrict__ out,
                                                         const uint32_t* __restrict__ kp) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -192,59 +193,37 @@ __global__ __launch_bounds__(256, 2) void ctr_bs_kernel(CtrBsArgs a, const u32x4
     const uint64_t b0 = ch * 2048u + lane;
     uint32_t s[128];
     // counter blocks -> planes (plane 32 w + r = bit r of word w = bit r % 8 of state byte
-    // 4 w + r / 8; bit j of a plane = block j).  When no 32-bit carry falls inside the chunk
-    // (all but one chunk in 2^21), words 0-2 are the chunk's own constants — their planes are
-    // 0 / ~0 — and only word 3 is transposed (fewer live registers than four transposes)
+    // 4 w + r / 8; bit j of a plane = block j).  The host gives this kernel only chunks without a
+    // 32-bit carry inside (ctr_launch), so words 0-2 are the chunk's constants — planes 0 / ~0 —
+    // and only word 3 is transposed
     const uint64_t c_lo = a.ctr_lo + ch * 2048u;  // the chunk's first counter (low half)
     const uint64_t c_hi = a.ctr_hi + (c_lo < a.ctr_lo ? 1u : 0u);
-    if ((uint32_t)c_lo <= 0xffffffffu - 2047u) {
-      const uint32_t w0 = __builtin_bswap32((uint32_t)(c_hi >> 32)), w1 = __builtin_bswap32((uint32_t)c_hi),
-                     w2 = __builtin_bswap32((uint32_t)(c_lo >> 32));
+    const uint32_t w0 = __builtin_bswap32((uint32_t)(c_hi >> 32)), w1 = __builtin_bswap32((uint32_t)c_hi),
+                   w2 = __builtin_bswap32((uint32_t)(c_lo >> 32));
 #pragma unroll
-      for (int r = 0; r < 32; ++r) {
-        s[r] = (w0 >> r) & 1u ? 0xffffffffu : 0u;
-        s[32 + r] = (w1 >> r) & 1u ? 0xffffffffu : 0u;
-        s[64 + r] = (w2 >> r) & 1u ? 0xffffffffu : 0u;
-      }
-      const uint32_t l0 = (uint32_t)c_lo + lane;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) s[96 + j] = __builtin_bswap32(l0 + 64u * (uint32_t)j);
-      bs_transpose32(s + 96);
-    } else {  // a 32-bit carry inside the chunk: every word per block
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-          uint32_t w0, w1, w2, w3;
-          ctr_words(a.ctr_hi, a.ctr_lo, b0 + 64u * (uint64_t)j, w0, w1, w2, w3);
-          s[32 * w + j] = w == 0 ? w0 : w == 1 ? w1 : w == 2 ? w2 : w3;
-        }
-        bs_transpose32(s + 32 * w);
-      }
+    for (int r = 0; r < 32; ++r) {
+      s[r] = (w0 >> r) & 1u ? 0xffffffffu : 0u;
+      s[32 + r] = (w1 >> r) & 1u ? 0xffffffffu : 0u;
+      s[64 + r] = (w2 >> r) & 1u ? 0xffffffffu : 0u;
     }
+    const uint32_t l0 = (uint32_t)c_lo + lane;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) s[96 + j] = __builtin_bswap32(l0 + 64u * (uint32_t)j);
+    bs_transpose32(s + 96);
 #pragma unroll
     for (int p = 0; p < 128; ++p) s[p] ^= kp[p];
 #pragma unroll 1
     for (int r = 1; r < 10; ++r) bs::round_mid(s, kp + 128 * r);
     bs::round_last(s, kp + 128 * 10);
-    // keystream out: s[32 w + j] = word w of block j's keystream after the four transposes; the
-    // blocks leave as 16-byte XORs in four batches of 8 (the compiler barrier keeps a batch's loads
-    // from being hoisted over the previous batch's stores: all 32 in flight took 128 more
-    // registers and spilled, two batches of 16 still spilled 17)
+    // keystream out: s[32 w + j] = word w of block j's keystream after the four transposes
 #pragma unroll
     for (int w = 0; w < 4; ++w) bs_transpose32(s + 32 * w);
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      u32x4 v[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int j = 8 * h + jj;
-        v[jj] = u32x4{s[j], s[32 + j], s[64 + j], s[96 + j]};
-        if (in) v[jj] ^= in[b0 + 64u * (uint64_t)j];
-      }
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) out[b0 + 64u * (uint64_t)(8 * h + jj)] = v[jj];
-      asm volatile("" ::: "memory");
+    for (int j = 0; j < 32; ++j) {
+      const uint64_t b = b0 + 64u * (uint64_t)j;
+      u32x4 v = {s[j], s[32 + j], s[64 + j], s[96 + j]};
+      if constexpr (XOR_IN) v ^= in[b];
+      out[b] = v;
     }
   }
 }
