@@ -7,9 +7,11 @@
  * a kernel launch, the staging of the tables and the host's completion wait.  With the service
  * started, single GCM messages from host memory — cmpi_gcm_seal_host / cmpi_gcm_open_host with
  * nrec = 1 and len <= 512 KiB, and therefore the EVP drop-in's per-message calls — are handed to a
- * kernel that stays resident on 8 CUs with its tables in LDS, polls a page-locked request word and
- * writes a page-locked completion word.  Outputs, statuses and errors are those of the calls it
- * serves (bit-exact; forged messages zero-filled, CMPI_EAUTH).
+ * kernel that stays resident on 8 CUs with its tables in LDS, polls a page-locked request ring and
+ * writes one page-locked completion slot per workgroup that served the message (its share of the
+ * tag); the host combines the slots into the tag, writes a seal's and checks an open's.  Outputs,
+ * statuses and errors are those of the calls it serves (bit-exact; forged messages zero-filled,
+ * CMPI_EAUTH).
  *
  * The kernel returns its CUs after `idle_us` microseconds without a message (0 = 2000) and at
  * least every 100 ms; the next message relaunches it.  While it runs it occupies 8 CUs: large
