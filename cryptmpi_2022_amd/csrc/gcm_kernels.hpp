@@ -469,6 +469,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
 constexpr uint32_t kFlowAgg = 147456u;         // aggregation slots, 16 x 16 B partials + 16 x 4 B records
 constexpr uint32_t kFlowLds = kFlowAgg + 512u;
 constexpr uint32_t kFlowFail = kFlowAgg + 448u;  // one-workgroup open: per-slot failed record + 1
+
 __device__ __forceinline__ uint32_t flow_tab(uint32_t f) {  // nibble table f (keysetup_kernels.hpp flow_nib_exp)
   return f < 8u ? f * 8192u : 131072u + (f - 8u) * 8192u;
 }
@@ -673,7 +674,8 @@ __device__ __forceinline__ u32x4 flow_unit(const GcmArgs& a, const RoundKeys& rk
   const bool j0_step0 = !SEP && i == 0u && base < 0;
   u32x4 ekj = {0u, 0u, 0u, 0u};
   for (uint32_t k = 0; k < steps; k += 2u) {
-    rotate_prio(it++);
+    rotate_prio(it++);  // (progress_prio here — the lane kernel's — was slower: 8 x 1 MiB seal
+                        // 19.43 -> 20.36 us, profiles/r05ao_flow_pprio_*.txt)
     const u32x4 ks = keystream(k == 0u && j0_step0 && lane == 0u ? 1u : ctr_of(k));
     if (k == 0u) ekj = ks;
     if (k == 0u) ustamp(28u);  // first keystream done (cache fill + one AES pass)
