@@ -478,7 +478,9 @@ __device__ __forceinline__ uint32_t flow_tab(uint32_t f) {  // nibble table f (k
 // (80 KiB), all loads issued before any LDS store (one L2 round trip).  (Measured, not taken:
 // building the nibble tables in LDS from their ten multipliers with nib_row_to_lds — 160 B fetched
 // instead of 80 KiB — staged at 5.4 us instead of 2.6 on 8 x 1 MiB: the 320 rows' VALU + 80 KiB
-// of ds_write_b128 cost more than the L2 round trip.)
+// of ds_write_b128 cost more than the L2 round trip.  Nor staging only the Horner's tables first
+// and the tree's 64 KiB from registers behind a barrier after the Horner: 8 x 1 MiB seal 19.67 ->
+// 20.15 us, profiles/r05aq_late_*.)
 // (stage_flow_tables: the loads and stores only, by threads 0..NT-1 — the resident service runs
 // more threads than it stages with; stage_flow adds the workgroup barrier.)
 template <int NT>
@@ -875,6 +877,9 @@ template <bool DECRYPT>
 __global__ __launch_bounds__(256) void gcm_xor_combine_kernel(GcmCombineArgs a) {
   const uint32_t r = blockIdx.x, t = threadIdx.x, lane = t & 63u;
   const u32x4* part = a.partial + (uint64_t)r * a.nseg;
+  // open: the received tag's load is issued with the partials' (its latency off the chain)
+  u32x4 tag = {0u, 0u, 0u, 0u};
+  if (DECRYPT && t == 0u) tag = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len);
   u32x4 y[4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
   uint32_t k = t;
   for (; k + 3u * 256u < a.nseg; k += 4u * 256u) {
@@ -891,7 +896,7 @@ __global__ __launch_bounds__(256) void gcm_xor_combine_kernel(GcmCombineArgs a) 
     if (!DECRYPT) {
       st_blk(a.out + (uint64_t)r * a.out_stride + a.len, v);
     } else {
-      const u32x4 d = ld_blk(a.in + (uint64_t)r * a.in_stride + a.len) ^ v;
+      const u32x4 d = tag ^ v;
       const uint32_t ok = ((d[0] | d[1] | d[2] | d[3]) == 0u) ? 1u : 0u;
       if (a.status) a.status[r] = (int32_t)ok;
       lds_st32(64u, ok);
