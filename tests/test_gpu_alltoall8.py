@@ -88,7 +88,7 @@ def _rank_main(rank: int, port: int, q) -> None:
         # (4) the bench's config-5 path at p = 8
         import bench
 
-        r = bench.alltoall_e2e(0, dist, dist.barrier, n=N, steps=2, warmup=1)
+        r = bench.alltoall_e2e(0, dist, dist.barrier, n=N, steps=2, warmup=1, warmup_s=0.05)
         res["bench_e2e"] = (r["ranks"] == WS and r["blocks_per_rank"] == WS and r["all_blocks_authenticated"]
                             and r["recv_matches_peers"] and r["parity_cpu"] and "gloo" in r["transport"])
         if not res["bench_e2e"]:

@@ -96,7 +96,7 @@ def test_bench_alltoall_e2e_one_rank(n):
     every block authenticates and the rank gets its own plaintext back."""
     import bench
 
-    res = bench.alltoall_e2e(0, None, lambda: None, n=n, steps=2, warmup=1)
+    res = bench.alltoall_e2e(0, None, lambda: None, n=n, steps=2, warmup=1, warmup_s=0.05)
     assert res["ranks"] == 1 and res["all_blocks_authenticated"] and res["recv_matches_peers"] and res["ms_per_call"] > 0
 
 
