@@ -733,7 +733,8 @@ def alltoall_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 100, w
             "parity": "every rank's wire blocks (nonce||ct||tag) vs OpenSSL 3 EVP_aes_128_gcm seal under the wire nonces"}
 
 
-def naive_collectives_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, warmup: int = 3) -> dict:
+def naive_collectives_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int = 20, warmup: int = 3,
+                          warmup_s: float = 0.1) -> dict:
     """The other naive secure collectives end to end at config 5's shape (p = 8 peers of 1 MiB;
     with fewer than 8 ranks each rank stands for 8/ranks of them, as alltoall_e2e): per call,
     one batched seal and one batched open per rank around the stock collective on the wire blocks
@@ -743,7 +744,9 @@ def naive_collectives_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int
       scatter    MPIR_Naive_Sec_Scatter (scatter.c:659-730): root seals 8, scatter, open own blocks
       bcast      MPI_Naive_Sec_Bcast (bcast.c:1510-1580): root seals 1, broadcast, the others open it
                  (one rank: it opens its own block)
-    Every rank runs this; time = MAX over ranks; statuses checked after the timed calls."""
+    Every rank runs this; time = MAX over ranks; statuses checked after the timed calls.  Before
+    each collective: `warmup_s` seconds of the rank's own batched seal + open (no collective: the
+    clocks' warm-up, as alltoall_e2e), then `warmup` whole calls."""
     from cryptmpi_2022_amd import _native as N
 
     p = pg.get_world_size() if pg is not None else 1
@@ -814,6 +817,12 @@ def naive_collectives_e2e(device: int, pg, barrier, n: int = 1 << 20, steps: int
     res = {"ranks": p, "block_bytes": n, "peers": tot, "root": 0,
            "transport": "RCCL (xGMI)" if p > 1 else "1 rank: device copy (blocks looped back)"}
     for name, fn in (("allgather", allgather), ("gather", gather), ("scatter", scatter), ("bcast", bcast)):
+        t_end = time.perf_counter() + warmup_s
+        while time.perf_counter() < t_end:
+            for _ in range(20):
+                seal(wire_all, send, tot)
+                opn(recv, wire_all, tot)
+            torch.cuda.synchronize(dev)
         for _ in range(warmup):
             fn()
         torch.cuda.synchronize(dev)
