@@ -701,6 +701,28 @@ def test_config5_shape_default_plan(nrec, n):
     assert np.array_equal(back[: nrec - 1], pt[: nrec - 1]) and not back[nrec - 1].any()
 
 
+@pytest.mark.parametrize("n,steps", [(1 << 20, 0), (64 * 16 * 3 - 5, 1)])
+def test_flow_combine_each_tag_byte(n, steps):
+    """gcm_xor_combine_kernel's tag check (the received tag is loaded beside the partials): 17
+    multi-chunk records, record i < 16 with tag byte i flipped, record 16 intact — each forged
+    record rejected and zero-filled, the intact one opened, whatever word of the tag differs."""
+    aead.force_wide(1, steps)
+    aead.set_flow_one_wg(False)
+    nrec = 17
+    ctx = aead.AeadCtx(KEY)
+    assert aead.gcm_plan(ctx, n, nrec)[1] > 1
+    pt = records(0x7A6 + n, nrec, n)
+    nonces = random_nonces(0x7A7 + n, nrec)
+    want = oracle.gcm_seal_batch(KEY, nonces, pt)
+    assert np.array_equal(gpu_seal(ctx, nonces, pt), want)
+    forged = want.copy()
+    for i in range(16):
+        forged[i, n + i] ^= 1 << (i % 8)
+    back, st = gpu_open(ctx, nonces, forged)
+    assert list(st) == [0] * 16 + [1]
+    assert not back[:16].any() and np.array_equal(back[16], pt[16])
+
+
 @pytest.mark.parametrize("n,nrec", [(32768, 16), (1 << 20, 8), (100000, 3), (65536 + 1, 1), (8 << 20, 1),
                                     (64 * 16 * 3 - 5, 7)])
 @pytest.mark.parametrize("threads", [0, 1024])
