@@ -71,12 +71,12 @@ def test_service_seal_open_vs_oracle(svc_ctx, pinned):
         st = np.full(1, 7, np.int32)
         assert _open(svc_ctx, back, ct, nonce, n, st) == N.CMPI_OK, n
         assert st[0] == 1 and back.tobytes() == pt.tobytes(), n
-        if n:  # a forged tag: status 0, plaintext zero-filled, CMPI_EAUTH
-            ct[n + 15] ^= 0x01
-            bad, _k4 = _host(n, pinned, fill=0x77)
-            st[0] = 7
-            assert _open(svc_ctx, bad, ct, nonce, n, st) == N.CMPI_EAUTH, n
-            assert st[0] == 0 and not bad.any(), n
+        # a forged tag (byte n % 16; an empty message too): status 0, plaintext zero-filled, CMPI_EAUTH
+        ct[n + n % 16] ^= 0x01
+        bad, _k4 = _host(n, pinned, fill=0x77)
+        st[0] = 7
+        assert _open(svc_ctx, bad, ct, nonce, n, st) == N.CMPI_EAUTH, n
+        assert st[0] == 0 and not bad.any(), n
     # the oracle's bit-serial GHASH between messages may outlast the 20 ms idle limit: the kernel
     # exits and the next message relaunches it
     src, _k1 = _host(64, pinned)
