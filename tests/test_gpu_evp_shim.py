@@ -83,6 +83,26 @@ def test_ctypes_seal_open_semantics():
     assert back.raw[:333] == bytes(333) and olen.value == 0
     # AAD is not supported by the drop-in (CryptMPI never passes any)
     assert L.EVP_AEAD_CTX_seal(ctx, out, ctypes.byref(olen), 349, nonce, 12, pt, 333, b"ad", 2) == 0
+    # rejected inputs (aead.h:251-253, :276-278): an input shorter than the tag, a nonce of other
+    # than 12 bytes, an output too small for the plaintext — 0, out zeroed, out_len 0
+    back = ctypes.create_string_buffer(b"\x22" * 333)
+    olen.value = 5
+    assert L.EVP_AEAD_CTX_open(ctx, back, ctypes.byref(olen), 333, nonce, 12, out.raw[:15], 15, None, 0) == 0
+    assert back.raw[:333] == bytes(333) and olen.value == 0
+    assert L.EVP_AEAD_CTX_seal(ctx, out, ctypes.byref(olen), 349, nonce, 8, pt, 333, None, 0) == 0
+    assert out.raw[:349] == bytes(349) and olen.value == 0
+    assert L.EVP_AEAD_CTX_seal(ctx, out, ctypes.byref(olen), 349, nonce, 12, pt, 333, None, 0) == 1
+    assert L.EVP_AEAD_CTX_open(ctx, back, ctypes.byref(olen), 332, nonce, 12, out.raw, 349, None, 0) == 0
+    assert back.raw[:332] == bytes(332) and olen.value == 0
+    # the empty message: tag only
+    tag = ctypes.create_string_buffer(16)
+    assert L.EVP_AEAD_CTX_seal(ctx, tag, ctypes.byref(olen), 16, nonce, 12, b"", 0, None, 0) == 1
+    assert olen.value == 16 and tag.raw[:16] == oracle.gcm_seal(key, nonce, b"")
+    assert L.EVP_AEAD_CTX_open(ctx, back, ctypes.byref(olen), 0, nonce, 12, tag.raw[:16], 16, None, 0) == 1
+    assert olen.value == 0
+    ftag = bytearray(tag.raw[:16])
+    ftag[7] ^= 0x40
+    assert L.EVP_AEAD_CTX_open(ctx, back, ctypes.byref(olen), 0, nonce, 12, bytes(ftag), 16, None, 0) == 0
     L.EVP_AEAD_CTX_free(ctx)
 
 
