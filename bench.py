@@ -1329,7 +1329,9 @@ def main() -> None:
     ap.add_argument("--workload", default="gcm1k", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
-    ap.add_argument("--serial", action="store_true", help="time only the one-stream pass (no two-stream pass)")
+    ap.add_argument("--serial", action="store_true", help="time only the one-stream pass (the default since round 6)")
+    ap.add_argument("--with-pipelined", action="store_true",
+                    help="also time the two-stream overlapped pass (reported as ms_per_step_pipelined)")
     ap.add_argument("--pipelined", action="store_true", help="headline = the two-stream overlapped pass")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank plumbing only (no GPU), for tests")
     args = ap.parse_args()
@@ -1370,13 +1372,15 @@ def main() -> None:
     wall, seal_ms, open_ms = time_steps(w, args.steps, args.warmup, barrier, warmup_s=WARMUP_S)
     ok = w.verify()
     wall_serial = wall
-    # the headline is this one-stream pass (each step seals then opens its batch).  Also timed:
-    # the same K steps with consecutive batches overlapped on two streams (seal of batch i+1 while
-    # batch i opens, the round-3 headline) — at steady state it is no faster (config 2: 0.1220 vs
-    # 0.1196 ms per step, profiles/r05r_*), so it is reported beside the headline, not as it;
-    # --pipelined makes it the headline.
+    # the headline is this one-stream pass (each step seals then opens its batch).  On request
+    # (--with-pipelined / --pipelined) also timed: the same K steps with consecutive batches
+    # overlapped on two streams (seal of batch i+1 while batch i opens, the round-3 headline) — at
+    # steady state it is no faster (config 2: 0.1220 vs 0.1196 ms per step, profiles/r05r_*).  Not
+    # run by default since round 6: its overlapped seal launches take twice as long each and mixed
+    # into a rocprofv3 summary of the default run they pulled the dominant kernel's average away
+    # from the serial launches this line's roofline is computed from.
     wall_pipe = None
-    if w.alg in ("gcm", "ocb") and not args.serial:
+    if w.alg in ("gcm", "ocb") and (args.pipelined or args.with_pipelined) and not args.serial:
         wall_pipe, ok_p = time_steps_pipelined(w, args.steps, args.warmup, barrier, warmup_s=0.2)
         ok = ok and ok_p
         if args.pipelined:

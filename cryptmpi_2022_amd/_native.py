@@ -128,7 +128,6 @@ _SIGS = {
     "cmpi_debug_force_wide": ([_I, _U32], None),
     "cmpi_debug_set_flow_threads": ([_I], None),
     "cmpi_debug_set_ctr_wg_per_cu": ([_I], None),
-    "cmpi_debug_set_ctr_hybrid": ([ctypes.c_uint64, _I], None),
     "cmpi_debug_set_lane_pair": ([_I], None),
     "cmpi_debug_set_svc_ls_min": ([_I], None),
     "cmpi_debug_set_flow_one_wg": ([_I], None),

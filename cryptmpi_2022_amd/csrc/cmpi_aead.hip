@@ -109,9 +109,6 @@ struct DevTables {
   // nibble tables of H^1,2,3,4,8,12,16,32,48,64: gcm_flow_kernel (all ten), lane-group weights
   // H^1..H^3 (the first three)
   uint8_t fnib[10][kNibTab];
-  // key planes of the bitsliced CTR kernel (ctr_bs_kernel): round r, plane p = bit p % 8 of byte
-  // p / 8 of round key r (rounds 1-9: of InvMixColumns(round key r)), as 0 / ~0
-  uint32_t bsk[11][128];
 };
 
 // Columns of the squaring maps X -> X^(2^i) (key setup of device-derived keys), once per process.
@@ -177,11 +174,6 @@ struct cmpi_ctx {
   mutable uint8_t* stage = nullptr;
   mutable size_t stage_cap = 0;
   mutable hipStream_t hstream = nullptr;
-  // the bitsliced share of a long CTR stream (ctr_launch): its stream, fork / join events, and the
-  // mutex that keeps one call's fork-join whole
-  mutable std::mutex bs_mu;
-  mutable hipStream_t bs_st = nullptr;
-  mutable hipEvent_t bs_fork = nullptr, bs_join = nullptr;
   mutable std::mutex hmu;                 // host-path pipeline (aead_host)
   std::unique_ptr<HostPipe> pipe{new HostPipe()};
   // the last device re-key (cmpi_ctx_rekey / _rekey_subkey) on the caller's stream: the library's
@@ -1211,13 +1203,6 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
 }
 
 std::atomic<int> g_ctr_wg_per_cu{2};  // cmpi_debug_set_ctr_wg_per_cu (co-residence experiments)
-// Long CTR streams: this share (per mille) of the whole 2 048-block chunks goes to the bitsliced
-// kernel (VALU) on the context's second stream while ctr_kernel (LDS) runs the rest at one
-// workgroup per CU; streams from g_ctr_hybrid_min bytes (cmpi_debug_set_ctr_hybrid).  Off by
-// default: the timing probe ran 1 572 vs 1 444 GiB/s at 15 % (r05ae), the product kernel — spill-
-// free, 715 GiB/s alone — 1 399 vs 1 392-1 397, parity (r05am_ctr_hybrid_sweep.jsonl).
-std::atomic<uint64_t> g_ctr_hybrid_min{(uint64_t)64 << 20};
-std::atomic<int> g_ctr_hybrid_permille{0};
 
 int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, const uint8_t ctr[16],
                       void* stream) {
@@ -1238,42 +1223,7 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   a.te0 = c->dt->te0;
   a.rk = folded(c->rk);
   a.sched = kSched;
-  int wg_per_cu = g_ctr_wg_per_cu.load();
-  // the bitsliced share: whole 2 048-block chunks from the stream's start
-  const int pm = g_ctr_hybrid_permille.load();
-  uint64_t bs_chunks = n >= g_ctr_hybrid_min.load() && pm > 0 ? (n / 16) * (uint64_t)pm / 1000u / 2048u : 0;
-  {  // the bitsliced kernel takes no chunk with a 32-bit counter carry inside: stop before the first
-    const uint64_t lo = cmpi::be64(ctr + 8);
-    const uint64_t to_carry = (0x100000000ull - (lo & 0xffffffffull)) / 2048u;  // whole chunks before it
-    if (bs_chunks > to_carry) bs_chunks = to_carry;
-  }
-  std::unique_lock<std::mutex> bs_lk(c->bs_mu, std::defer_lock);
-  if (bs_chunks) {
-    bs_lk.lock();  // this call's fork / join on the context's second stream
-    if (!c->bs_st) HIP_TRY(lib_stream(&c->bs_st));
-    if (!c->bs_fork) HIP_TRY(hipEventCreateWithFlags(&c->bs_fork, hipEventDisableTiming));
-    if (!c->bs_join) HIP_TRY(hipEventCreateWithFlags(&c->bs_join, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(c->bs_fork, st));  // the caller's earlier work first
-    HIP_TRY(hipStreamWaitEvent(c->bs_st, c->bs_fork, 0));
-    cmpi::dev::CtrBsArgs b{};
-    b.nchunks = bs_chunks;
-    b.ctr_hi = a.ctr_hi;
-    b.ctr_lo = a.ctr_lo;
-    const dim3 bsg((uint32_t)std::min<uint64_t>(bs_chunks, (uint64_t)c->ncu));
-    const u32x4* bin = reinterpret_cast<const u32x4*>(in);
-    u32x4* bout = reinterpret_cast<u32x4*>(out);
-    const uint32_t* bkp = c->dt->bsk[0];
-    HIP_TRY(in ? launch_k(cmpi::dev::ctr_bs_kernel<true>, bsg, dim3(256), 0, c->bs_st, b, bin, bout, bkp)
-               : launch_k(cmpi::dev::ctr_bs_kernel<false>, bsg, dim3(256), 0, c->bs_st, b, bin, bout, bkp));
-    const uint64_t skip = bs_chunks * 2048u, sb = skip * 16u;  // the T-table kernel takes the rest
-    a.in = in ? in + sb : nullptr;
-    a.out = out + sb;
-    a.n = n - sb;
-    const uint64_t lo = a.ctr_lo + skip;
-    a.ctr_hi += lo < a.ctr_lo ? 1u : 0u;
-    a.ctr_lo = lo;
-    wg_per_cu = 1;  // half the CU's VGPRs for the bitsliced waves
-  }
+  const int wg_per_cu = g_ctr_wg_per_cu.load();
   a.nblk = (a.n + 15) / 16;
   const uint64_t blocks = (a.nblk + 1023) / 1024;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->ncu * (uint64_t)wg_per_cu));
@@ -1282,10 +1232,6 @@ int ctr_launch(const cmpi_ctx* c, uint8_t* out, const uint8_t* in, size_t n, con
   int rc = set_lds_attr(reinterpret_cast<const void*>(fn), c->device, lds);
   if (rc) return rc;
   HIP_TRY(launch_k(fn, dim3(grid), dim3(1024), lds, st, a));
-  if (bs_chunks) {  // the caller's stream continues after both shares
-    HIP_TRY(hipEventRecord(c->bs_join, c->bs_st));
-    HIP_TRY(hipStreamWaitEvent(st, c->bs_join, 0));
-  }
   return CMPI_OK;
 }
 
@@ -1397,25 +1343,6 @@ cmpi_ctx* cmpi_ctx_new(int alg, const uint8_t* key, size_t key_len, size_t tag_l
     for (uint32_t f = 0; f < cmpi::dev::kFlowNib; ++f)
       cmpi::build_nibble_table(cmpi::gf_pow(c->H, cmpi::dev::flow_nib_exp(f)), reinterpret_cast<Blk*>(ht->fnib[f]));
   }
-  {  // bitsliced key planes (ctr_bs_kernel)
-    auto xt = [](uint32_t x) { return ((x << 1) ^ ((x & 0x80u) ? 0x1bu : 0u)) & 0xffu; };
-    auto gm = [&](uint32_t a, int m) {  // a · m in GF(2^8), m in {9, 11, 13, 14}
-      const uint32_t a2 = xt(a), a4 = xt(a2), a8 = xt(a4);
-      return (a8 ^ ((m & 4) ? a4 : 0u) ^ ((m & 2) ? a2 : 0u) ^ ((m & 1) ? a : 0u)) & 0xffu;
-    };
-    for (int r = 0; r < 11; ++r) {
-      uint8_t k[16], kin[16];
-      for (int b = 0; b < 16; ++b) k[b] = (uint8_t)(c->rk.w[4 * r + b / 4] >> (8 * (b % 4)));
-      for (int col = 0; col < 4; ++col)
-        for (int row = 0; row < 4; ++row) {
-          const uint8_t* a = k + 4 * col;
-          kin[4 * col + row] = (r == 0 || r == 10) ? a[row]
-                               : (uint8_t)(gm(a[row], 14) ^ gm(a[(row + 1) % 4], 11) ^ gm(a[(row + 2) % 4], 13) ^
-                                           gm(a[(row + 3) % 4], 9));
-        }
-      for (int p = 0; p < 128; ++p) ht->bsk[r][p] = ((kin[p / 8] >> (p % 8)) & 1u) ? 0xffffffffu : 0u;
-    }
-  }
   if (alg == CMPI_AES_128_OCB) {
     // RFC 7253 §4.1: L_* = E_K(0), L_$ = double(L_*), L_0 = double(L_$), L_i = double(L_{i-1})
     auto dbl = [](const uint8_t* in, uint8_t* o) {
@@ -1457,7 +1384,6 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   if (c->pipe && c->pipe->init)
     for (auto& ps : c->pipe->s) (void)hipStreamSynchronize(ps);
   if (c->hstream) (void)hipStreamSynchronize(c->hstream);
-  if (c->bs_st) (void)hipStreamSynchronize(c->bs_st);
   if (c->scratch_used) (void)hipEventSynchronize(c->scratch_ev);
   if (c->scratch_ev) (void)hipEventDestroy(c->scratch_ev);
   if (c->key_ev) {
@@ -1472,9 +1398,6 @@ void cmpi_ctx_free(cmpi_ctx* c) {
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->stage) (void)hipFree(c->stage);
   if (c->hstream) (void)hipStreamDestroy(c->hstream);
-  if (c->bs_st) (void)hipStreamDestroy(c->bs_st);
-  if (c->bs_fork) (void)hipEventDestroy(c->bs_fork);
-  if (c->bs_join) (void)hipEventDestroy(c->bs_join);
   if (c->pipe) {
     HostPipe& P = *c->pipe;
     if (P.init) {
@@ -1530,10 +1453,6 @@ void cmpi_debug_set_svc_ls_min(int ls) { g_svc_ls_min.store(ls >= 0 && ls <= 3 ?
 void cmpi_debug_set_lane_pair(int on) { g_lane_pair.store(on >= 1 && on <= 4 ? on : 0); }
 void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 || threads == 1024 ? threads : 0); }
 void cmpi_debug_set_ctr_wg_per_cu(int n) { g_ctr_wg_per_cu.store(n >= 1 && n <= 2 ? n : 2); }
-void cmpi_debug_set_ctr_hybrid(uint64_t min_bytes, int permille) {
-  g_ctr_hybrid_min.store(min_bytes);
-  g_ctr_hybrid_permille.store(permille < 0 ? 0 : permille > 1000 ? 1000 : permille);
-}
 
 // Timing events without the system-scope release fence (hipEventDisableSystemFence): a default
 // event's fence writes back and invalidates the caches and leaves a ~6 us bubble before the

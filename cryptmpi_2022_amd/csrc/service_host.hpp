@@ -235,8 +235,10 @@ int svc_stop_locked(Svc& S) {
 
 // Stop and free the context's service (hmu held).  If the stop failed (its launch event could not
 // be waited), the generation may still be resident: its memory is freed only once its exit word
-// shows it left (200 ms bound); otherwise it is left allocated — a leak, never a
-// kernel polling or writing freed memory.
+// shows it left (200 ms bound).  Otherwise the whole Svc is left allocated — its
+// device words, and the object itself, which a stream slot may still name as its owner: the next
+// svc_launch on that slot reads the owner's exit word and writes its kick word, so neither may be
+// freed (a leak, never a kernel or a host thread touching freed memory).
 int svc_shutdown_locked(cmpi_ctx* c) {
   if (!c->svc) return CMPI_OK;
   Svc& S = *c->svc;
@@ -245,8 +247,10 @@ int svc_shutdown_locked(cmpi_ctx* c) {
   for (const auto t0 = std::chrono::steady_clock::now();
        !gone && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200);)
     gone = svc_exited(S);
-  if (gone) svc_release(S);
-  delete c->svc;
+  if (gone) {
+    svc_release(S);  // clears every slot that names it
+    delete c->svc;
+  }
   c->svc = nullptr;
   return rc;
 }
@@ -262,7 +266,7 @@ int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc]
     if (int rc = svc_launch(c, S, S.seq)) return rc;
   const uint32_t seq = ++S.seq;
   svc_post(S, d, seq);
-  const uint32_t ngrp = svc_groups(d[0], d[1], S.ls_min);
+  uint32_t ngrp = svc_groups(d[0], d[1], S.ls_min);
   const auto t0 = std::chrono::steady_clock::now();
   int relaunches = 0;
   for (uint32_t i = 1;; ++i) {
@@ -273,6 +277,7 @@ int svc_exec(const cmpi_ctx* c, Svc& S, const uint32_t (&d)[cmpi::dev::kSvcDesc]
       if (svc_done(S, seq, ngrp, w)) break;
       if (++relaunches > 2) return fail(CMPI_EHIP, "message service did not complete message %u", seq);
       if (int rc = svc_launch(c, S, seq - 1)) return rc;  // it never saw the message
+      ngrp = svc_groups(d[0], d[1], S.ls_min);  // the new generation's chunk plan
       continue;
     }
     if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {

@@ -44,10 +44,6 @@ void cmpi_debug_set_flow_threads(int threads);
 /* ctr_kernel workgroups per CU (1 or 2; default 2 = every VGPR of the CU): 1 leaves room for a
  * co-resident kernel (tools/probe/hybrid_ctr_probe.hip). */
 void cmpi_debug_set_ctr_wg_per_cu(int n);
-/* Long CTR streams (cmpi_ctr_xor / cmpi_ctr_keystream of at least min_bytes; default 64 MiB):
- * permille of the whole 2 048-block chunks run on the bitsliced kernel beside ctr_kernel (default
- * 0 = T-table only: the hybrid is an experiment). */
-void cmpi_debug_set_ctr_hybrid(uint64_t min_bytes, int permille);
 /* gcm_lane_kernel (L = 4) record stores grouped by 128-byte output line (each line stored whole in
  * the step that completes it), on batches of at least one group per thread of the grid: 2 =
  * predicated selects (default), 1 = branches, 0 = a store per step; 3 / 4 = the select / branch

@@ -74,34 +74,26 @@ def test_ctr_config4_full_stream(ctr_lo):
     assert np.array_equal(host(out), oracle.ctr_xor_mt(KEY, iv, pt.cpu().numpy()))
 
 
-@pytest.mark.parametrize("permille", [1000, 400, 150])
 @pytest.mark.parametrize("cb_hex", ["fffffffffffffffffffffffffffff000", "000102030405060708090a0bfffff7f0",
                                     "f0f1f2f3f4f5f6f7f8f9fafbfcfdfeff"])
-def test_ctr_hybrid_bitsliced_share(permille, cb_hex):
-    """The bitsliced CTR kernel (ctr_bs_kernel, VALU AES) on its share of a stream beside ctr_kernel
-    (cmpi_debug_set_ctr_hybrid forces it on short streams): every byte vs the oracle, counters
-    carrying across 32 / 64 / 128 bits inside a chunk, XOR, in place and keystream-only."""
-    from cryptmpi_2022_amd import _native as N
-
-    L = N.lib()
-    L.cmpi_debug_set_ctr_hybrid(0, permille)
-    try:
-        cb = bytes.fromhex(cb_hex)
-        ctx = aead.CipherCtx(KEY, "aes-128-ctr")
-        n = 5 * 2048 * 16 + 13  # five whole 2 048-block chunks and a ragged tail
-        pt = splitmix64_bytes(0x51 + permille, n)
-        want = oracle.ctr_xor_mt(KEY, cb, pt)
-        out = empty(n)
-        ctx.ctr_xor(out, dev(pt), n, cb)
-        assert np.array_equal(host(out)[:n], want)
-        ctx.ctr_xor(out, out, n, cb)  # in place: back to the plaintext
-        assert np.array_equal(host(out)[:n], pt)
-        nb = n // 16
-        ks = empty(nb * 16)
-        ctx.keystream(ks, nb, cb)
-        assert host(ks)[: nb * 16].tobytes() == oracle.ctr_xor(KEY, cb, bytes(nb * 16))
-    finally:
-        L.cmpi_debug_set_ctr_hybrid(64 << 20, 0)
+def test_ctr_carry_corners_chunks(cb_hex):
+    """Counters carrying across 32 / 64 / 128 bits inside a 2 048-block chunk: every byte vs the
+    oracle, XOR, in place and keystream-only (the bitsliced share this test also covered in round 5
+    left the product library in round 6)."""
+    cb = bytes.fromhex(cb_hex)
+    ctx = aead.CipherCtx(KEY, "aes-128-ctr")
+    n = 5 * 2048 * 16 + 13  # five whole 2 048-block chunks and a ragged tail
+    pt = splitmix64_bytes(0x51, n)
+    want = oracle.ctr_xor_mt(KEY, cb, pt)
+    out = empty(n)
+    ctx.ctr_xor(out, dev(pt), n, cb)
+    assert np.array_equal(host(out)[:n], want)
+    ctx.ctr_xor(out, out, n, cb)  # in place: back to the plaintext
+    assert np.array_equal(host(out)[:n], pt)
+    nb = n // 16
+    ks = empty(nb * 16)
+    ctx.keystream(ks, nb, cb)
+    assert host(ks)[: nb * 16].tobytes() == oracle.ctr_xor(KEY, cb, bytes(nb * 16))
 
 
 def test_ctr_keystream_equals_xor_of_zeros():

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Generator of cryptmpi_2022_amd/csrc/aes_bitslice_gen.hpp (ctr_kernels.hpp ctr_bs_kernel, tools/probe/*): bitsliced AES-128 rounds for gfx950
+"""Generator of tools/probe/aes_bitslice_gen.hpp (tools/probe/ctr_bs_kernel.hpp and the probes; out of the product library since round 6): bitsliced AES-128 rounds for gfx950
 as v_bitop3_b32 (3-input LUT) networks.
 
-Bitsliced layout (csrc/aes_bitslice.hpp): a lane's 32-bit register holds ONE bit of the state
+Bitsliced layout: a lane's 32-bit register holds ONE bit of the state
 of 32 blocks (bit j of the register = block j).  Plane p = 8*i + b is bit b (b = 0 the LSB) of
 state byte i (FIPS-197 byte order, column-major: byte i sits in column i/4, row i%4).  A round
 is then a straight-line network of bitwise ops over 128 planes.
@@ -535,8 +535,7 @@ def bop1(args, tt):
 def main():
     gates = parse_bp()
     check_bp(gates)
-    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cryptmpi_2022_amd", "csrc",
-                            "aes_bitslice_gen.hpp")
+    out_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "probe", "aes_bitslice_gen.hpp")
     parts = ["// aes_bitslice_gen.hpp — GENERATED by tools/gen_bitslice.py; do not edit.\n"
              "// Bitsliced AES-128 rounds as gfx950 v_bitop3_b32 networks (ctr_kernels.hpp ctr_bs_kernel).\n"
              "#pragma once\n#include <stdint.h>\n\nnamespace cmpi::bs {\n\n"

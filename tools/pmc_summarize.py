@@ -4,7 +4,9 @@ profiles/pmc_<wl>.json: per-kernel average counters and, for the dominant seal k
 traffic per launch corrected as MI355X_MICROARCH.md §HBM prescribes:
   FETCH_SIZE (KiB) reports 1/2 of a 16-B-per-lane streaming read on gfx950 -> x2;
   WRITE_SIZE (KiB) is exact for 16-B-per-lane streaming stores.
-Usage: tools/pmc_summarize.py <workload> <pmc dir> <kernel substring>"""
+Only the last LAST launches of each kernel per pass are averaged (env LAST, default 0 = all): with
+tools/prof_driver.py's time-based warm-up those are the sustained serial launches bench.py times.
+Usage: [LAST=N] tools/pmc_summarize.py <workload> <pmc dir> <kernel substring>"""
 import collections
 import csv
 import glob
@@ -15,14 +17,27 @@ import sys
 wl, d, ksub = sys.argv[1], sys.argv[2], sys.argv[3]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 durs = collections.defaultdict(list)
+LAST = int(os.environ.get("LAST", "0"))
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
+    rows = collections.defaultdict(list)  # kernel -> [(start, dispatch, counter, value, duration)]
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         if "cmpi::dev" not in name:
             continue
         short = name.split("(")[0].replace("void cmpi::dev::", "")
-        agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
-        durs[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+        rows[short].append((int(r["Start_Timestamp"]), r.get("Dispatch_Id", ""), r["Counter_Name"],
+                            float(r["Counter_Value"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
+    for short, rs in rows.items():
+        starts = sorted({x[0] for x in rs})
+        keep = set(starts[-LAST:]) if LAST else set(starts)
+        seen = set()
+        for st, disp, c, v, du in rs:
+            if st not in keep:
+                continue
+            agg[short][c].append(v)
+            if (st, disp) not in seen:
+                seen.add((st, disp))
+                durs[short].append(du)
 out = {"workload": wl, "source": d, "round": os.environ.get("ROUND", "round unrecorded"), "kernels": {}}
 for k, cs in agg.items():
     avg = {c: sum(v) / len(v) for c, v in cs.items()}

@@ -10,7 +10,7 @@
 #include <stdint.h>
 #include <stdio.h>
 
-#include "../../cryptmpi_2022_amd/csrc/aes_bitslice_gen.hpp"
+#include "aes_bitslice_gen.hpp"
 
 template <int TPB>
 __global__ __launch_bounds__(TPB) void bs_ctr(const uint32_t* __restrict__ kp, uint32_t* __restrict__ out, uint32_t nonce0,

@@ -15,7 +15,7 @@
 
 #include "../../include/cmpi_aead.h"
 #include "../../include/cmpi_debug.h"
-#include "../../cryptmpi_2022_amd/csrc/aes_bitslice_gen.hpp"
+#include "aes_bitslice_gen.hpp"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 

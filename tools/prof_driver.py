@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Minimal driver for rocprofv3 (kernel-trace / PMC passes): runs `iters` seal+open steps of one
-bench workload on cuda:0, nothing else (no distributed init, no CPU baseline)."""
+bench workload on cuda:0, nothing else (no distributed init, no CPU baseline).  The steps follow
+--warmup-s seconds of untimed steps (default 0.5, as bench.py's headline), so that the last
+`iters` launches of each kernel are the sustained, serial ones bench.py times; summarise only those
+(tools/pmc_summarize.py LAST=<iters>, tools/rocprof_split.py --last <iters>)."""
 import argparse
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -15,6 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="gcm1k")
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--seal-only", action="store_true")
+ap.add_argument("--warmup-s", type=float, default=0.5)
 ap.add_argument("--out-stride", type=int, default=0,
                 help="gcm1k seal-only traffic calibration: output record stride (0 = dense n+16)")
 a = ap.parse_args()
@@ -37,6 +42,13 @@ if a.out_stride:  # 65 536 x 1 KiB seals into records `out_stride` bytes apart (
     print("ok out_stride", a.out_stride)
     sys.exit(0)
 w = Workload(a.workload, 0, seed=1)
+t_end = time.perf_counter() + a.warmup_s
+while time.perf_counter() < t_end:
+    for _ in range(10):
+        w.seal()
+        if not a.seal_only:
+            w.open()
+    torch.cuda.synchronize()
 for _ in range(a.iters):
     w.seal()
     if not a.seal_only:

@@ -1,37 +1,55 @@
 #!/usr/bin/env python3
 """Per-launch durations from a rocprofv3 --kernel-trace CSV (run_kernel_trace.csv), split per
-kernel and grid size (the grid tells the bench workloads apart): count, mean and median in us.
-usage: rocprof_split.py <run_kernel_trace.csv> [title]"""
+kernel, grid size and schedule phase: count, mean and median in us.
+
+A phase is a run of launches of one (kernel, grid) with no gap longer than --gap-ms between two
+consecutive launches.  bench.py separates its workloads by CPU-side parity checks that take far
+longer than that, so each phase is one workload's pass (the headline's untimed first step, its
+warm-up + timed steps, the gcm4k extra, ...), told apart by when they ran rather than by how long
+each launch took.  Phases shorter than --min-n launches are folded into one "other" line.
+
+usage: rocprof_split.py <run_kernel_trace.csv> [title] [--gap-ms 20] [--min-n 50]"""
+import argparse
 import collections
 import csv
-import sys
 
 
 def main() -> None:
-    path = sys.argv[1]
-    agg = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("void cmpi::dev::", "")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("title", nargs="?")
+    ap.add_argument("--gap-ms", type=float, default=20.0)
+    ap.add_argument("--min-n", type=int, default=50)
+    a = ap.parse_args()
+    launches = collections.defaultdict(list)  # (name, grid) -> [(start_ns, dur_us)]
+    for r in csv.DictReader(open(a.csv)):
         if "cmpi::dev" not in r["Kernel_Name"]:
             continue
+        name = r["Kernel_Name"].split("(")[0].replace("void cmpi::dev::", "")
         grid = r.get("Grid_Size_X") or r.get("Grid_Size") or "?"
-        agg[(name, grid)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
-    if len(sys.argv) > 2:
-        print(sys.argv[2])
-    for (name, grid), v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        launches[(name, grid)].append((s, (e - s) * 1e-3))
+    if a.title:
+        print(a.title)
+    gap = a.gap_ms * 1e6
+    for (name, grid), v in sorted(launches.items(), key=lambda kv: -sum(d for _, d in kv[1])):
         v.sort()
-        groups = [v]
-        if len(v) > 20 and v[len(v) * 9 // 10] > 2.5 * v[len(v) // 10]:  # two workloads on one grid
-            lo, hi = v[len(v) // 10], v[len(v) * 9 // 10]
-            for _ in range(20):  # 2-means on the durations
-                cut = (lo + hi) / 2
-                a, b = [x for x in v if x < cut], [x for x in v if x >= cut]
-                lo, hi = sum(a) / len(a), sum(b) / len(b)
-            groups = [a, b]
-        for gi, g in enumerate(groups):
-            tag = "" if len(groups) == 1 else f" cluster {gi}"
-            print(f"{name:44s} grid={grid:>8s}{tag:10s} n={len(g):6d} mean={sum(g) / len(g):9.2f} "
-                  f"median={g[len(g) // 2]:9.2f}")
+        phases, cur = [], [v[0]]
+        for prev, x in zip(v, v[1:]):
+            if x[0] - prev[0] > gap:
+                phases.append(cur)
+                cur = []
+            cur.append(x)
+        phases.append(cur)
+        big = [p for p in phases if len(p) >= a.min_n]
+        small = [x for p in phases if len(p) < a.min_n for x in p]
+        rows = [(f"phase {i}", p) for i, p in enumerate(big)] + ([("other", small)] if small else [])
+        t0 = v[0][0]
+        for tag, p in rows:
+            d = sorted(x for _, x in p)
+            when = "" if tag == "other" else f" t={(p[0][0] - t0) * 1e-9:7.3f}s"
+            print(f"{name:44s} grid={grid:>8s} {tag:8s}{when:11s} n={len(d):6d} mean={sum(d) / len(d):9.2f} "
+                  f"median={d[len(d) // 2]:9.2f}")
 
 
 if __name__ == "__main__":
