@@ -376,12 +376,16 @@ def time_steps_pipelined(w: Workload, steps: int, warmup: int, barrier, warmup_s
     return wall, ok
 
 
-def time_steps(w: Workload, steps: int, warmup: int, barrier, warmup_s: float = 0.0):
-    """Returns (wall seconds for `steps` steps, avg seal kernel ms, avg open kernel ms) —
-    kernel times from HIP events recorded on the stream the kernels are launched on, around every
-    seal and open launch of the timed region (fence-free events, KernelEvents).  The warm-up is
-    `warmup` steps and, when warmup_s > 0, at least that many seconds of them (the extras run
-    after the CPU baseline has left the GPU idle for seconds: clocks ramp back up first)."""
+def time_steps(w: Workload, steps: int, warmup: int, barrier, warmup_s: float = 0.0, detail: dict | None = None):
+    """Returns (wall seconds for `steps` steps, avg seal kernel ms, avg open kernel ms).  Kernel
+    times: HIP events on the stream the kernels are launched on, for every seal and open launch of
+    the timed region — the kernel's own start / stop events (hipExtLaunchKernel through
+    cmpi_debug_time_next_launch: the execution rocprofv3 reports).  Also recorded (into `detail`):
+    the stream bracket, fence-free events recorded between the launches (KernelEvents), which
+    holds each launch's dispatch gap after the previous kernel as well; the two brackets of a step
+    sum to its wall time.  The warm-up is `warmup` steps and, when warmup_s > 0, at least that many
+    seconds of them (the extras run after the CPU baseline has left the GPU idle for seconds:
+    clocks ramp back up first)."""
     t_w = time.perf_counter()
     i = 0
     while i < warmup or time.perf_counter() - t_w < warmup_s:
@@ -394,21 +398,29 @@ def time_steps(w: Workload, steps: int, warmup: int, barrier, warmup_s: float = 
     assert w.verify(), "round trip failed in warm-up"
     stream = torch.cuda.current_stream(w.dev).cuda_stream
     ev = KernelEvents(2 * steps + 1)
+    kev = KernelEvents(4 * steps)  # per launch: start, stop of the kernel itself
+    timed = kev.L.cmpi_debug_time_next_launch
     barrier()
     torch.cuda.synchronize(w.dev)
     t0 = time.perf_counter()
     ev.record(0, stream)
     for i in range(steps):
+        timed(kev.ev[4 * i], kev.ev[4 * i + 1])
         w.seal()
         ev.record(2 * i + 1, stream)
+        timed(kev.ev[4 * i + 2], kev.ev[4 * i + 3])
         w.open()
         ev.record(2 * i + 2, stream)
     torch.cuda.synchronize(w.dev)
     barrier()
     wall = time.perf_counter() - t0
-    seal_ms = sum(ev.ms(2 * i, 2 * i + 1) for i in range(steps)) / steps
-    open_ms = sum(ev.ms(2 * i + 1, 2 * i + 2) for i in range(steps)) / steps
+    seal_ms = sum(kev.ms(4 * i, 4 * i + 1) for i in range(steps)) / steps
+    open_ms = sum(kev.ms(4 * i + 2, 4 * i + 3) for i in range(steps)) / steps
+    if detail is not None:
+        detail["seal_ms_stream_bracket"] = sum(ev.ms(2 * i, 2 * i + 1) for i in range(steps)) / steps
+        detail["open_ms_stream_bracket"] = sum(ev.ms(2 * i + 1, 2 * i + 2) for i in range(steps)) / steps
     ev.free()
+    kev.free()
     return wall, seal_ms, open_ms
 
 
@@ -1369,7 +1381,8 @@ def main() -> None:
     w.open()
     assert w.verify(), "round trip failed"
     # W warm-up steps, and at least WARMUP_S seconds of them (clocks out of their idle state)
-    wall, seal_ms, open_ms = time_steps(w, args.steps, args.warmup, barrier, warmup_s=WARMUP_S)
+    tdet: dict = {}
+    wall, seal_ms, open_ms = time_steps(w, args.steps, args.warmup, barrier, warmup_s=WARMUP_S, detail=tdet)
     ok = w.verify()
     wall_serial = wall
     # the headline is this one-stream pass (each step seals then opens its batch).  On request
@@ -1420,7 +1433,14 @@ def main() -> None:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": f"seal launch ({kname})",
-                     "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bpl},
+                     "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bpl,
+                     "kernel_ms_timing": ("hipExtLaunchKernel start/stop events of each seal launch of the timed "
+                                          "region (the kernel's execution, as rocprofv3 --kernel-trace reports it)"),
+                     "launch_ms_stream_bracket": round(tdet["seal_ms_stream_bracket"], 4),
+                     "launch_ms_stream_bracket_note": ("fence-free events recorded on the stream between the "
+                                                       "launches: the kernel plus the dependent launch's dispatch "
+                                                       "gap; seal + open brackets = the step's wall time"),
+                     "frac_stream_bracket": round(bpl / (tdet["seal_ms_stream_bracket"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "lds_roofline": lds_roofline(w, kern_ms, local) if w.alg == "gcm" else None,
         "verified_round_trip": ok,
         "parity_cpu": None if parity is None else parity["parity_cpu"],

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import re
 
 try:  # share torch's HIP runtime when torch is present
@@ -138,6 +139,7 @@ _SIGS = {
     "cmpi_debug_event_record": ([_P, _P], _I),
     "cmpi_debug_event_ms": ([_P, _P], ctypes.c_float),
     "cmpi_debug_event_free": ([_P], None),
+    "cmpi_debug_time_next_launch": ([_P, _P], None),
     "cmpi_debug_set_host_chunk": ([_S], None),
     "cmpi_debug_gcm_plan": ([_P, _S, _S, _P], _I),
     "cmpi_debug_set_stream_mode": ([_I], None),
@@ -161,14 +163,21 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')"
             )
         L = ctypes.CDLL(LIB_PATH)
-        # an A/B build of an older revision (CMPI_LIB, tools/ab_build.sh) may lack newer hooks
-        lenient = bool(os.environ.get("CMPI_LIB"))
+        # an A/B build of an older revision (tools/ab_build.sh, compared by the A/B tools, which set
+        # CMPI_LIB_LENIENT=1) may lack newer hooks: those are skipped and named on stderr.  Any other
+        # library — the product, or the diagnostics build loaded through CMPI_LIB — must export
+        # every symbol, so a stale build fails here rather than at a call site.
+        lenient = os.environ.get("CMPI_LIB_LENIENT") == "1"
+        skipped = []
         for name, (args, res) in _SIGS.items():
             fn = getattr(L, name, None) if lenient else getattr(L, name)
             if fn is None:
+                skipped.append(name)
                 continue
             fn.argtypes = args
             fn.restype = res
+        if skipped:
+            sys.stderr.write(f"cryptmpi_2022_amd: {LIB_PATH} lacks {', '.join(skipped)} (CMPI_LIB_LENIENT=1)\n")
         for name, (args, res) in _TOOLS_SIGS.items():
             fn = getattr(L, name, None)
             if fn is not None:

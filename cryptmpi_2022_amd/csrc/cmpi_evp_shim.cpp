@@ -19,6 +19,9 @@
 //    keeps inside its own; without one the call fails (returns 0) instead of misreading it.
 #include <sys/random.h>
 #include <dlfcn.h>
+#include <link.h>
+#include <unistd.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -81,12 +84,14 @@ size_t env_size(const char* name, size_t dflt) {
 }
 const size_t kIdleCap = env_size("CMPI_EVP_CTX_CACHE", 16);
 const long kWindowUs = (long)env_size("CMPI_EVP_COALESCE_US", 30);
-// CMPI_EVP_SERVICE_US = n > 0: every context serves its single messages from the resident message
-// service (include/cmpi_service.h), which returns its CUs after n us without messages — the AEAD
-// contexts' seal / open and the CTR / ECB cipher contexts' EVP_EncryptUpdate of up to 64 KiB (the
-// 700 / 702 per-message calls, the 602 sub-key derivation).  0 (default): one kernel launch per
-// EVP call.
-const size_t kServiceUs = env_size("CMPI_EVP_SERVICE_US", 0);
+// CMPI_EVP_SERVICE_US = n > 0 (default 2000): every context serves its single messages from the
+// resident message service (include/cmpi_service.h), which returns its CUs after n us without
+// messages — the AEAD contexts' seal / open and the CTR / ECB cipher contexts' EVP_EncryptUpdate of
+// up to 64 KiB (the 700 / 702 per-message calls, the 602 sub-key derivation).  0: one kernel launch
+// per EVP call.  On by default since round 6: a launch per call costs a 64 KiB seal + open 57.6 us
+// against 24 served, more than one CPU core's 25; while idle the kernel holds
+// 8 CUs for at most n us (capped at 20 ms) and then leaves.
+const size_t kServiceUs = env_size("CMPI_EVP_SERVICE_US", 2000);
 // idle limit of the drop-in's services: a resident kernel delays device-wide synchronisation
 // (hipDeviceSynchronize) of the whole process until it idles out (cmpi_service.h)
 constexpr size_t kServiceCapUs = 20000;
@@ -230,6 +235,80 @@ void release(Shared* s) {
   for (Shared* o : evict) destroy(o);
 }
 
+// ---------------------------------------------------------------- static message buffers
+// CryptMPI seals into and opens from its own static arrays (large_send_buffer / large_recv_buffer,
+// mpiimpl.h:292-293, 64 MiB each in libmpi's .bss; send.c:311, recv.c:322).  Page-locked, the
+// engine's kernels read and write them in place over PCIe; pageable, every byte goes through the
+// service's bounce buffer (a memcpy each way).  Static storage of an object loaded at program start
+// is never unmapped, so the shim page-locks such a segment, whole and once, the first time a
+// message touches it — the registration can never outlive the memory (what makes a general
+// pin-down cache of user buffers unsafe without allocator hooks: freed and re-mapped pages).
+// CMPI_EVP_REGISTER_STATIC = 0 turns it off; segments above CMPI_EVP_REGISTER_STATIC_MAX bytes
+// (default 1 GiB) are left pageable.
+struct StaticSeg {
+  uintptr_t lo, hi;  // whole pages inside one writable PT_LOAD segment
+  std::once_flag once;
+  bool ok = false;
+};
+struct StaticSegs {
+  std::vector<StaticSeg*> v;
+};
+const size_t kRegStatic = env_size("CMPI_EVP_REGISTER_STATIC", 1);
+const size_t kRegStaticMax = env_size("CMPI_EVP_REGISTER_STATIC_MAX", (size_t)1 << 30);
+
+int collect_seg(struct dl_phdr_info* info, size_t, void* arg) {
+  auto* segs = static_cast<StaticSegs*>(arg);
+  const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+  uintptr_t relro_end = 0;  // the start of a writable segment turns read-only after relocation
+  for (int i = 0; i < info->dlpi_phnum; ++i)
+    if (info->dlpi_phdr[i].p_type == PT_GNU_RELRO)
+      relro_end = info->dlpi_addr + info->dlpi_phdr[i].p_vaddr + info->dlpi_phdr[i].p_memsz;
+  for (int i = 0; i < info->dlpi_phnum; ++i) {
+    const ElfW(Phdr)& ph = info->dlpi_phdr[i];
+    if (ph.p_type != PT_LOAD || !(ph.p_flags & PF_W)) continue;
+    uintptr_t a = info->dlpi_addr + ph.p_vaddr;
+    const uintptr_t b = a + ph.p_memsz;
+    if (relro_end > a && relro_end < b) a = relro_end;
+    // whole writable pages only: the first may share a page with the RELRO (read-only) part
+    const uintptr_t lo = (a + pg - 1) & ~(pg - 1), hi = (b + pg - 1) & ~(pg - 1);
+    if (hi > lo && hi - lo <= kRegStaticMax) {
+      auto* s = new StaticSeg();
+      s->lo = lo;
+      s->hi = hi;
+      segs->v.push_back(s);
+    }
+  }
+  return 0;
+}
+
+// The writable segments of the objects loaded when the shim was (program start for a DT_NEEDED
+// libmpi); never freed.
+const StaticSegs& static_segs() {
+  static const StaticSegs* s = [] {
+    auto* x = new StaticSegs();
+    if (kRegStatic) dl_iterate_phdr(collect_seg, x);
+    return x;
+  }();
+  return *s;
+}
+__attribute__((constructor)) void snapshot_static_segs() { (void)static_segs(); }
+
+// [p, p + n) inside a static segment: page-lock that segment (once; a failure leaves it pageable).
+void register_static(const void* p, size_t n) {
+  if (!kRegStatic || !p || n < 4096) return;  // small messages: the bounce copy is cheaper
+  const uintptr_t a = (uintptr_t)p, b = a + n;
+  for (StaticSeg* s : static_segs().v)
+    if (a >= s->lo && b <= s->hi) {
+      std::call_once(s->once, [s] {
+        s->ok = cmpi_host_register((void*)s->lo, s->hi - s->lo) == CMPI_OK;
+        if (getenv("CMPI_EVP_DEBUG"))
+          fprintf(stderr, "cmpi_evp: static segment [%#lx, %#lx) %zu bytes page-locked: %s\n", (unsigned long)s->lo,
+                  (unsigned long)s->hi, (size_t)(s->hi - s->lo), s->ok ? "yes" : "no");
+      });
+      return;
+    }
+}
+
 bool ensure_stage(Shared* s, size_t need) {
   if (need <= s->stage_cap) return true;
   if (s->stage) {
@@ -253,6 +332,8 @@ void run_group(Shared* s, Req** r, size_t k, bool open) {
   const size_t n = r[0]->len;
   if (k == 1) {
     int32_t st = 0;
+    register_static(r[0]->in, open ? n + 16 : n);
+    register_static(r[0]->out, open ? n : n + 16);
     if (!open)
       r[0]->ok = cmpi_gcm_seal_host(s->c, r[0]->out, 0, r[0]->in ? r[0]->in : r[0]->out, 0, r[0]->nonce, 12, n, 1) == CMPI_OK;
     else

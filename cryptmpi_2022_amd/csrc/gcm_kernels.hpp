@@ -244,6 +244,10 @@ __device__ __forceinline__ void build_byte_table(const u32x4* __restrict__ src, 
 #ifndef CMPI_PRIO_EVERY
 #define CMPI_PRIO_EVERY 1
 #endif
+// record loads / stores of the full-block loop: MEM bit 0 non-temporal loads, bit 1 stores
+#ifndef CMPI_LANE_MEM
+#define CMPI_LANE_MEM 0
+#endif
 template <int L, bool DECRYPT, int PAIR>
 __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
   CMPI_PROBE(a, 0u);
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
     const uint8_t* ip = in_rec + 16u * x0;
     uint8_t* op = out_rec + 16u * x0;
     if (nfull > 0u) {
-      auto ld = [&](uint32_t uu) { return ld_blk(ip + 16u * (uu < nfull ? uu : nfull - 1u)); };
+      auto ld = [&](uint32_t uu) { return ld_rec<CMPI_LANE_MEM>(ip + 16u * (uu < nfull ? uu : nfull - 1u)); };
       if constexpr (PAIR != 0 && L == 4) {
         // Line-aligned stores: a 128-byte line of the output holds 8 blocks, two group steps.  The
         // group's blocks are computed in order as always; each lane keeps its outputs of the last
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
         u32x4 vn = CMPI_LANE_PREFETCH >= 2 ? ld(q + 4u) : u32x4{0u, 0u, 0u, 0u};
         u32x4 vnn = CMPI_LANE_PREFETCH >= 3 ? ld(q + 8u) : u32x4{0u, 0u, 0u, 0u};
         auto put = [&](int32_t b, u32x4 x) {
-          if (b >= 0 && b < nf) st_blk(op + 16u * (uint32_t)b, x);
+          if (b >= 0 && b < nf) st_rec<CMPI_LANE_MEM>(op + 16u * (uint32_t)b, x);
         };
 #pragma unroll CMPI_LANE_UNROLL
         for (uint32_t k = 0; k < nsteps; ++k) {
@@ -342,8 +346,8 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
             const bool cur = (int32_t)q + j <= 7;
             const int32_t ba = cur ? u - 4 : u - 8;
             const u32x4 xa = cur ? h1 : h2, xb = cur ? o : h1;
-            if (j >= 4 && ba >= 0) st_blk(op + 16u * (uint32_t)ba, xa);
-            if (j >= 4 && ba + 4 >= 0 && ba + 4 < nf) st_blk(op + 16u * (uint32_t)(ba + 4), xb);
+            if (j >= 4 && ba >= 0) st_rec<CMPI_LANE_MEM>(op + 16u * (uint32_t)ba, xa);
+            if (j >= 4 && ba + 4 >= 0 && ba + 4 < nf) st_rec<CMPI_LANE_MEM>(op + 16u * (uint32_t)(ba + 4), xb);
           }
           h2 = h1;
           h1 = o;
@@ -374,7 +378,7 @@ __global__ __launch_bounds__(1024) void gcm_lane_kernel(GcmArgs a) {
         for (uint32_t u = q; u < nfull; u += (uint32_t)L) {
           progress_prio(gcm_prog_off(L), ++done);
           const u32x4 o = v ^ keystream(2u + x0 + u);
-          st_blk(op + 16u * u, o);
+          st_rec<CMPI_LANE_MEM>(op + 16u * u, o);
           acc = gmul_byte(acc, gl, DECRYPT ? v : o);
           v = ld(u + (uint32_t)L);
         }

@@ -29,9 +29,14 @@ extern "C" {
 /* Seal with fresh nonces, the RAND_bytes + seal pair fused into the seal kernel itself:
  * nonce_r = P || BE64(c + r), P 4 bytes and the counter's start value 8 bytes drawn from the OS
  * CSPRNG when the context was created, c advanced by nrec per call — the deterministic
- * construction of SP 800-38D §8.2.1 with a random fixed field: a context never repeats a nonce,
- * and two contexts under one key (ranks sharing CryptMPI's global key) collide only if their
- * random fields and counter ranges both meet.  Nonces are written at nonce_out + r*nonce_stride. */
+ * construction of SP 800-38D §8.2.1 with a random fixed field: a context never repeats a nonce
+ * (its counter is 64 bits wide and advances under an atomic).  Across contexts under one key (ranks
+ * sharing CryptMPI's global key) uniqueness is probabilistic, not assigned: two contexts repeat a
+ * nonce only if their random 4-byte fields are equal (2^-32 per pair) AND their counter ranges
+ * overlap (about (N1 + N2) / 2^64 for N1, N2 nonces drawn from random 64-bit starts) — below 2^-80
+ * per pair for any realistic N, so for p ranks below p^2 · 2^-81.  This matches what CryptMPI's
+ * RAND_bytes(nonce, 12) per message gives (send.c:294; a birthday bound over 96 random bits).
+ * Nonces are written at nonce_out + r*nonce_stride. */
 int cmpi_gcm_seal_batch_fresh(const cmpi_ctx *ctx, uint8_t *out, size_t out_stride, const uint8_t *in,
                               size_t in_stride, uint8_t *nonce_out, size_t nonce_stride, size_t len, size_t nrec,
                               void *workspace, void *stream);

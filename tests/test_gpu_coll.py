@@ -70,6 +70,24 @@ def test_fresh_nonce_construction():
     assert bytes(host(wire)[:4]) != ctrs[0][0]
 
 
+def test_fresh_nonces_disjoint_across_contexts():
+    """Sixteen contexts under one key (ranks sharing CryptMPI's global key) seal 64 blocks each
+    twice: all 2 048 nonces are distinct, each context keeps one random field (the bound
+    across contexts is probabilistic, include/cmpi_coll.h)."""
+    ctxs = [aead.AeadCtx(KEY) for _ in range(16)]
+    seen, fields = set(), set()
+    for rnd in range(2):
+        for k, c in enumerate(ctxs):
+            wire = empty(64 * 28, fill=0)
+            coll.seal_blocks(c, wire, empty(1), 0, 64)
+            w = host(wire)[: 64 * 28].reshape(64, 28)
+            nonces = {bytes(x[:12]) for x in w}
+            assert len(nonces) == 64 and not (nonces & seen), (rnd, k)
+            seen |= nonces
+            fields.add(bytes(w[0, :4]))
+    assert len(seen) == 2 * 16 * 64 and len(fields) == 16
+
+
 def test_two_rank_alltoall_in_process():
     """Rank r seals p blocks for its peers, block (r -> q) travels to rank q, q opens it."""
     p, n = 2, 4096

@@ -32,8 +32,7 @@ def test_c_client_naive_alltoall(tmp_path, p, n, service):
     inp.write_bytes(key + nonces.tobytes() + send.tobytes())
     outp = tmp_path / "out.bin"
     env = dict(os.environ)
-    if service:
-        env["CMPI_EVP_SERVICE_US"] = "2000"
+    env["CMPI_EVP_SERVICE_US"] = "2000" if service else "0"  # 0: a kernel launch per call
     r = subprocess.run([str(exe), str(p), str(n), str(inp), str(outp)], capture_output=True, text=True, env=env,
                        timeout=120)
     assert r.returncode == 0, (r.returncode, r.stderr)
@@ -126,8 +125,8 @@ def test_c_client_threads_share_one_ctx(tmp_path, threads, msgs, n, service):
     inp, outp = tmp_path / "in.bin", tmp_path / "out.bin"
     inp.write_bytes(key + nonces.tobytes() + pt.tobytes())
     env = dict(os.environ)
-    if service:  # single messages served by each context's resident kernel (CMPI_EVP_SERVICE_US)
-        env["CMPI_EVP_SERVICE_US"] = "2000"
+    # single messages served by each context's resident kernel, or a kernel launch per call
+    env["CMPI_EVP_SERVICE_US"] = "2000" if service else "0"
     r = subprocess.run([str(exe), str(threads), str(msgs), str(n), str(inp), str(outp)], capture_output=True,
                        text=True, timeout=120, env=env)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)

@@ -43,7 +43,16 @@ def child(workload: str) -> None:
     torch.cuda.synchronize()
     seal = sum(ev.ms(2 * i, 2 * i + 1) for i in range(iters)) / iters * 1e3
     opn = sum(ev.ms(2 * i + 1, 2 * i + 2) for i in range(iters)) / iters * 1e3
-    print(json.dumps({"seal_us": seal, "open_us": opn, "step_ms": (seal + opn) / 1e3, "ok": bool(w.verify())}))
+    # the same steps with no event between the launches (two events around the whole run)
+    ev.record(0, st)
+    for i in range(iters):
+        w.seal()
+        w.open()
+    ev.record(1, st)
+    torch.cuda.synchronize()
+    bare = ev.ms(0, 1) / iters * 1e3
+    print(json.dumps({"seal_us": seal, "open_us": opn, "step_ms": (seal + opn) / 1e3, "step_us_no_events": bare,
+                      "ok": bool(w.verify())}))
 
 
 def main() -> None:
@@ -59,7 +68,7 @@ def main() -> None:
     for _ in range(rounds):
         for lib in libs:
             path, _, hooks = lib.partition("@")
-            env = dict(os.environ, CMPI_LIB=os.path.abspath(path), AB_HOOKS=hooks)
+            env = dict(os.environ, CMPI_LIB=os.path.abspath(path), CMPI_LIB_LENIENT="1", AB_HOOKS=hooks)
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", workload], env=env,
                                capture_output=True, text=True, timeout=120)
             if p.returncode != 0:
@@ -72,8 +81,9 @@ def main() -> None:
     for lib in libs:
         s = sorted(r["seal_us"] for r in runs[lib])
         o = sorted(r["open_us"] for r in runs[lib])
+        b = sorted(r["step_us_no_events"] for r in runs[lib])
         res[lib] = {"seal_us": round(s[len(s) // 2], 2), "open_us": round(o[len(o) // 2], 2),
-                    "ok": all(r["ok"] for r in runs[lib])}
+                    "step_us_no_events": round(b[len(b) // 2], 2), "ok": all(r["ok"] for r in runs[lib])}
     print(json.dumps({"workload": workload, "rounds": rounds, "medians": res}))
 
 
