@@ -1207,6 +1207,42 @@ def c_timed_latency(iters: int = 300) -> dict:
     return out
 
 
+def c_pingpong_600(iters: int = 2000) -> dict:
+    """CryptMPI's per-message 600 exchange between two processes, in C, through the BoringSSL ABI
+    (tools/evp_pingpong.c: send.c:221-337 / recv.c:219-341 framing, shared-memory transport,
+    static large_send/recv_buffer, malloc'd user buffers): one-way latency medians of the plaintext
+    exchange, the secure one through libcmpi_evp.so (the drop-in's defaults: resident service on;
+    and with CMPI_EVP_SERVICE_US=0, a kernel launch per call) and through OpenSSL 3 on the calling
+    core; crypto_added = secure - plaintext."""
+    import subprocess
+
+    gpu, cpu = os.path.join(ROOT, "tools", "evp_pingpong"), os.path.join(ROOT, "tools", "evp_pingpong_ossl")
+    if not (os.path.exists(gpu) and os.path.exists(cpu)):
+        return {"error": "tools/evp_pingpong not built (make -C tools pingpong)"}
+
+    def run(exe, mode, n, env=None):
+        p = subprocess.run([exe, mode, str(n), str(iters)], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, **(env or {})))
+        if p.returncode != 0:
+            raise RuntimeError(f"{os.path.basename(exe)} {mode} {n}: rc {p.returncode} {p.stderr[-300:]}")
+        d = json.loads(p.stdout.strip().splitlines()[-1])
+        assert d["verified"], "ping-pong payload mismatch"
+        return d["oneway_us_median"]
+
+    out = {"iters": iters, "unit": "us one-way (round trip / 2), median"}
+    for n in (1024, 65536):
+        k = f"{n // 1024}k"
+        plain = run(gpu, "plain", n)
+        served = run(gpu, "secure", n)
+        launch = run(gpu, "secure", n, {"CMPI_EVP_SERVICE_US": "0"})
+        ossl = run(cpu, "secure", n)
+        out[k] = {"plain_us": plain, "secure_dropin_us": served, "secure_dropin_launch_per_call_us": launch,
+                  "secure_openssl_1core_us": ossl, "crypto_added_dropin_us": round(served - plain, 2),
+                  "crypto_added_dropin_launch_per_call_us": round(launch - plain, 2),
+                  "crypto_added_openssl_1core_us": round(ossl - plain, 2)}
+    return out
+
+
 def cpu_port_baseline(workload: str, seconds: float = 4.0) -> dict:
     """Secondary CPU datum: the oracle's C restatement (portable table AES, bit-serial GHASH;
     oracle/liboracle.so), all usable host threads, on a bounded sample of the workload."""
@@ -1499,7 +1535,8 @@ def main() -> None:
         except Exception as e:
             extras["host_602_8mib"] = {"error": repr(e)}
         for name, fn in (("async_host", lambda: async_host_rate(local)), ("ctr702", lambda: ctr702_rates(local)),
-                         ("config1_exchange_64k", config1_exchange), ("c_timed_latency", c_timed_latency)):
+                         ("config1_exchange_64k", config1_exchange), ("c_timed_latency", c_timed_latency),
+                         ("c_pingpong_600", c_pingpong_600)):
             try:
                 extras[name] = fn()
             except Exception as e:  # report, never hide
