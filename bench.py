@@ -377,15 +377,19 @@ def time_steps_pipelined(w: Workload, steps: int, warmup: int, barrier, warmup_s
 
 
 def time_steps(w: Workload, steps: int, warmup: int, barrier, warmup_s: float = 0.0, detail: dict | None = None):
-    """Returns (wall seconds for `steps` steps, avg seal kernel ms, avg open kernel ms).  Kernel
-    times: HIP events on the stream the kernels are launched on, for every seal and open launch of
-    the timed region — the kernel's own start / stop events (hipExtLaunchKernel through
-    cmpi_debug_time_next_launch: the execution rocprofv3 reports).  Also recorded (into `detail`):
-    the stream bracket, fence-free events recorded between the launches (KernelEvents), which
-    holds each launch's dispatch gap after the previous kernel as well; the two brackets of a step
-    sum to its wall time.  The warm-up is `warmup` steps and, when warmup_s > 0, at least that many
-    seconds of them (the extras run after the CPU baseline has left the GPU idle for seconds:
-    clocks ramp back up first)."""
+    """Returns (wall seconds for `steps` steps, avg seal kernel ms, avg open kernel ms).
+
+    The timed region: `steps` steps, each sealing then opening the whole batch on one stream, with
+    fence-free HIP events (KernelEvents) recorded on that stream between the launches — its wall
+    clock is the headline; each launch's stream bracket (the kernel plus the dependent launch's
+    dispatch gap after the previous kernel; seal + open brackets = the step) goes into `detail`.
+    Kernel times: right after it, the same `steps` steps again with every seal and open launched
+    through hipExtLaunchKernel with start / stop events (cmpi_debug_time_next_launch) — the
+    kernel's own execution, what rocprofv3 --kernel-trace reports.  They are a pass of their own
+    because those events widen each launch's dispatch gap (config 2: ~4 us per launch, ~6 % of a
+    step, profiles/r06c_*), which the headline must not carry.  The warm-up is `warmup` steps and,
+    when warmup_s > 0, at least that many seconds of them (the extras run after the CPU baseline
+    has left the GPU idle for seconds: clocks ramp back up first)."""
     t_w = time.perf_counter()
     i = 0
     while i < warmup or time.perf_counter() - t_w < warmup_s:
@@ -398,29 +402,37 @@ def time_steps(w: Workload, steps: int, warmup: int, barrier, warmup_s: float = 
     assert w.verify(), "round trip failed in warm-up"
     stream = torch.cuda.current_stream(w.dev).cuda_stream
     ev = KernelEvents(2 * steps + 1)
-    kev = KernelEvents(4 * steps)  # per launch: start, stop of the kernel itself
-    timed = kev.L.cmpi_debug_time_next_launch
     barrier()
     torch.cuda.synchronize(w.dev)
     t0 = time.perf_counter()
     ev.record(0, stream)
     for i in range(steps):
-        timed(kev.ev[4 * i], kev.ev[4 * i + 1])
         w.seal()
         ev.record(2 * i + 1, stream)
-        timed(kev.ev[4 * i + 2], kev.ev[4 * i + 3])
         w.open()
         ev.record(2 * i + 2, stream)
     torch.cuda.synchronize(w.dev)
     barrier()
     wall = time.perf_counter() - t0
+    seal_br = sum(ev.ms(2 * i, 2 * i + 1) for i in range(steps)) / steps
+    open_br = sum(ev.ms(2 * i + 1, 2 * i + 2) for i in range(steps)) / steps
+    ev.free()
+    # kernel-timing pass (outside the timed region)
+    kev = KernelEvents(4 * steps)  # per launch: the kernel's start, stop
+    timed = kev.L.cmpi_debug_time_next_launch
+    for i in range(steps):
+        timed(kev.ev[4 * i], kev.ev[4 * i + 1])
+        w.seal()
+        timed(kev.ev[4 * i + 2], kev.ev[4 * i + 3])
+        w.open()
+    timed(None, None)
+    torch.cuda.synchronize(w.dev)
     seal_ms = sum(kev.ms(4 * i, 4 * i + 1) for i in range(steps)) / steps
     open_ms = sum(kev.ms(4 * i + 2, 4 * i + 3) for i in range(steps)) / steps
-    if detail is not None:
-        detail["seal_ms_stream_bracket"] = sum(ev.ms(2 * i, 2 * i + 1) for i in range(steps)) / steps
-        detail["open_ms_stream_bracket"] = sum(ev.ms(2 * i + 1, 2 * i + 2) for i in range(steps)) / steps
-    ev.free()
     kev.free()
+    if detail is not None:
+        detail["seal_ms_stream_bracket"] = seal_br
+        detail["open_ms_stream_bracket"] = open_br
     return wall, seal_ms, open_ms
 
 
@@ -1466,16 +1478,21 @@ def main() -> None:
                    "parallelism": f"records sharded, {ws} independent rank(s), no collective"},
         "seal_GiBps_per_gpu": round(per_rank_bytes / (seal_ms * 1e-3) / GIB, 2),
         "open_GiBps_per_gpu": round(per_rank_bytes / (open_ms * 1e-3) / GIB, 2),
+        "seal_GiBps_per_gpu_stream_bracket": round(per_rank_bytes / (tdet["seal_ms_stream_bracket"] * 1e-3) / GIB, 2),
+        "rates_note": ("seal/open GiBps from the kernels' own execution (hipExtLaunchKernel events, the kernel-"
+                       "timing pass); *_stream_bracket from the timed region's stream events, dispatch gaps "
+                       "included; value from the timed region's wall clock"),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": f"seal launch ({kname})",
                      "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bpl,
-                     "kernel_ms_timing": ("hipExtLaunchKernel start/stop events of each seal launch of the timed "
-                                          "region (the kernel's execution, as rocprofv3 --kernel-trace reports it)"),
+                     "kernel_ms_timing": ("hipExtLaunchKernel start/stop events of every seal launch of a pass of "
+                                          "`steps` steps run right after the timed region (the kernel's execution, "
+                                          "as rocprofv3 --kernel-trace reports it)"),
                      "launch_ms_stream_bracket": round(tdet["seal_ms_stream_bracket"], 4),
                      "launch_ms_stream_bracket_note": ("fence-free events recorded on the stream between the "
-                                                       "launches: the kernel plus the dependent launch's dispatch "
-                                                       "gap; seal + open brackets = the step's wall time"),
+                                                       "launches of the timed region: the kernel plus the dependent "
+                                                       "launch's dispatch gap; seal + open brackets = the step"),
                      "frac_stream_bracket": round(bpl / (tdet["seal_ms_stream_bracket"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "lds_roofline": lds_roofline(w, kern_ms, local) if w.alg == "gcm" else None,
         "verified_round_trip": ok,
@@ -1510,10 +1527,13 @@ def main() -> None:
         for name in ("gcm4k", "ocb1m", "ctr1g", "ctr1g_mask", "alltoall"):
             try:
                 we = Workload(name, local, seed=77)
-                wl, s_ms, o_ms = time_steps(we, EXTRA_STEPS, EXTRA_WARMUP, barrier, warmup_s=0.3)
+                edet: dict = {}
+                wl, s_ms, o_ms = time_steps(we, EXTRA_STEPS, EXTRA_WARMUP, barrier, warmup_s=0.3, detail=edet)
                 extras[name] = {"seal_open_GiBps": round(we.n * we.nrec * EXTRA_STEPS / wl / GIB, 2),
                                 "seal_GiBps": round(we.n * we.nrec / (s_ms * 1e-3) / GIB, 2),
                                 "open_GiBps": round(we.n * we.nrec / (o_ms * 1e-3) / GIB, 2),
+                                "seal_GiBps_stream_bracket": round(
+                                    we.n * we.nrec / (edet["seal_ms_stream_bracket"] * 1e-3) / GIB, 2),
                                 "seal_hbm_frac": round(we.bytes_per_launch() / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                 "verified": we.verify()}
                 par = we.parity_cpu()

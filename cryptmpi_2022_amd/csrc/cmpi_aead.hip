@@ -68,11 +68,22 @@ int fail(int code, const char* fmt, ...) {
 // caller's included — and clears it, so an unrelated earlier failure would fail the seal (and the
 // EVP shim put zeros on the wire) while the caller lost its own error.  hipLaunchKernel returns
 // the launch's status and leaves a pending error of the caller's alone.
-// Kernel timing for bench.py's roofline (cmpi_debug_time_next_launch): the next kernel this thread
-// launches goes through hipExtLaunchKernel with these start / stop events, which time that kernel
-// itself rather than the stream between two event records (a record bracket also holds the
-// dependent launch's dispatch gap after the previous kernel).
+// Kernel timing for bench.py's roofline (cmpi_debug_time_next_launch): the kernels this thread
+// launches go through hipExtLaunchKernel — the first with the start event, every one with the stop
+// event (a two-launch call, flow kernel + combine, is timed from the first kernel's start to the
+// last one's end) — until the hook is cleared.  These events time the kernels themselves rather
+// than the stream between two event records (a record bracket also holds the dependent launch's
+// dispatch gap after the previous kernel).
 thread_local hipEvent_t t_time_start = nullptr, t_time_stop = nullptr;
+
+hipError_t launch_raw(const void* fn, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t st) {
+  if (t_time_start || t_time_stop) {
+    const hipEvent_t e0 = t_time_start;
+    t_time_start = nullptr;
+    return hipExtLaunchKernel(fn, grid, block, args, lds, st, e0, t_time_stop, 0);
+  }
+  return hipLaunchKernel(fn, grid, block, args, lds, st);
+}
 
 template <class... P, class... A>
 hipError_t launch_k(void (*fn)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t st, A&&... a) {
@@ -81,12 +92,7 @@ hipError_t launch_k(void (*fn)(P...), dim3 grid, dim3 block, size_t lds, hipStre
   return std::apply(
       [&](auto&... x) {
         void* args[] = {static_cast<void*>(&x)...};
-        if (t_time_start || t_time_stop) {
-          const hipEvent_t e0 = t_time_start, e1 = t_time_stop;
-          t_time_start = t_time_stop = nullptr;
-          return hipExtLaunchKernel(reinterpret_cast<const void*>(fn), grid, block, args, lds, st, e0, e1, 0);
-        }
-        return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, block, args, lds, st);
+        return launch_raw(reinterpret_cast<const void*>(fn), grid, block, args, lds, st);
       },
       t);
 }
@@ -691,7 +697,7 @@ int gcm_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     const uint32_t wpb = (uint32_t)NT / 64u;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((waves + wpb - 1) / wpb, (uint64_t)c->ncu));
     void* kargs[] = {&a};
-    HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(NT), kargs, lds, st));
+    HIP_TRY(launch_raw(fn, dim3(grid), dim3(NT), kargs, lds, st));
     if (one_wg) return CMPI_OK;
     cmpi::dev::GcmCombineArgs ca{};
     ca.in = in;
@@ -1087,33 +1093,10 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
     return gcm_ws_bytes(c, plan_gcm(c, len, nr), nr);
   };
-  // Chunks: K records each, except that a batch of more than a few chunks starts and ends with a
-  // ramp K/8, K/4, K/2 (and back down): the pipeline's fill (the first chunk's H2D, nothing to
-  // overlap it) and drain (the last chunk's D2H) then cost an eighth of a chunk each instead of a
-  // whole one.  CMPI_HOST_RAMP=0: uniform chunks.
-  static const bool ramp_on = !getenv("CMPI_HOST_RAMP") || atoi(getenv("CMPI_HOST_RAMP")) != 0;
-  std::vector<std::pair<size_t, size_t>> chunks;  // (first record, records)
-  {
-    std::vector<size_t> ramp;
-    for (size_t k = K / 8; ramp_on && k >= 1 && k < K; k *= 2) ramp.push_back(k);
-    size_t rsum = 0;
-    for (size_t k : ramp) rsum += k;
-    if (ramp.empty() || nrec < 2 * rsum + 2 * K) {
-      for (size_t r0 = 0; r0 < nrec; r0 += K) chunks.emplace_back(r0, std::min(K, nrec - r0));
-    } else {
-      size_t r0 = 0;
-      for (size_t k : ramp) chunks.emplace_back(r0, k), r0 += k;
-      const size_t mid = nrec - 2 * rsum, nmid = (mid + K - 1) / K;
-      for (size_t i = 0; i < nmid; ++i) {
-        const size_t k = mid / nmid + (i < mid % nmid ? 1 : 0);
-        chunks.emplace_back(r0, k), r0 += k;
-      }
-      for (size_t i = ramp.size(); i-- > 0;) chunks.emplace_back(r0, ramp[i]), r0 += ramp[i];
-    }
-  }
-  size_t ws_max = 0;
-  for (const auto& ch : chunks) ws_max = std::max(ws_max, ws_for(ch.second));
-  const size_t ws_b = up16(ws_max);
+  // (Measured, not taken, round 6: chunks ramping K/8, K/4, K/2 up and back down around the 16 MiB
+  // ones, to shorten the pipeline's fill and drain — 33.0-33.7 GiB/s with or without, two
+  // alternated rounds on one box, profiles/r06c_host_ramp.jsonl.)
+  const size_t ws_b = up16(std::max(ws_for(K), ws_for(nrec - (nrec - 1) / K * K)));
   const size_t in_b = up2m(ip * K), out_b = up2m(op * K), n_b = up16(npitch * K), st_b = up16(4 * K);
   const size_t slot_b = up2m(in_b + out_b + n_b + st_b + ws_b);
   if (P.cap < slot_b || P.ns < NS) {
@@ -1146,7 +1129,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   // whole batch is enqueued at once and the three streams pipeline on events alone.
   const bool cpu_pack = (in_rec && !in_pinned) || !n_flat;
   const bool cpu_unpack = out_rec && !out_pinned;
-  const size_t nchunks = chunks.size();
+  const size_t nchunks = (nrec + K - 1) / K;
   static const bool dbg_sync = getenv("CMPI_DEBUG_SYNC") != nullptr;  // diagnose: sync + check each step
   auto step = [&](const char* what, size_t ci) -> int {
     if (!dbg_sync) return CMPI_OK;
@@ -1172,7 +1155,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   // copy chunk ci's outputs from the pinned slot to the user's buffers (after its D2H)
   auto unpack = [&](size_t ci) -> int {
     const int sl = (int)(ci % NS);
-    const size_t r0 = chunks[ci].first, nr = chunks[ci].second;
+    const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
     HIP_TRY(hipEventSynchronize(P.slot_free[sl]));
     const auto h = layout(sl, P.hbuf);
     par_copy_records(out + r0 * out_stride, out_stride, h.out, op, out_rec, nr);
@@ -1181,7 +1164,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   int rc = CMPI_OK;
   for (size_t ci = 0; ci < nchunks && !rc; ++ci) {
     const int sl = (int)(ci % NS);
-    const size_t r0 = chunks[ci].first, nr = chunks[ci].second;
+    const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
     const auto d = layout(sl, P.buf);
     const auto h = layout(sl, P.hbuf);
     // slot sl was last used by chunk ci-2: its H2D must have read the pinned inputs and its

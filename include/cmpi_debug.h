@@ -38,9 +38,10 @@ int cmpi_debug_copy(void* dst, const void* src, size_t n, void* stream);
 int cmpi_debug_event_record(void* ev, void* stream);
 float cmpi_debug_event_ms(void* a, void* b);
 void cmpi_debug_event_free(void* ev);
-/* The next kernel the calling thread launches through the library is timed by these two events
- * (hipExtLaunchKernel start / stop events: the kernel's own execution, as rocprofv3 reports it,
- * not the stream between two records); one-shot.  bench.py's roofline kernel time. */
+/* Kernel timing (bench.py's roofline): the kernels the calling thread launches through the library
+ * from now on go through hipExtLaunchKernel, the first with start_ev and each with stop_ev, so the
+ * pair times the next call's kernels themselves (first start to last end; rocprofv3's view), not
+ * the stream between two records.  (NULL, NULL) ends it. */
 void cmpi_debug_time_next_launch(void* start_ev, void* stop_ev);
 /* gcm_flow_kernel threads per workgroup: 0 automatic (always 512 since round 4: the 1024-thread
  * form spills), 512 or 1024 forced (the chunk plan then assumes that many waves per CU). */
