@@ -1563,7 +1563,10 @@ def main() -> None:
                 extras[name] = {"error": repr(e)}
         result["extras"] = extras
     if not args.no_extras:  # config 5 end to end: a collective, so every rank runs it
-        a2a = alltoall_e2e(local, pg, barrier)
+        try:
+            a2a = alltoall_e2e(local, pg, barrier)
+        except Exception as e:  # report, never hide (the headline above is already measured)
+            a2a = {"error": repr(e)}
         # the other collectives: on one rank by default (RCCL gather / scatter across ranks run
         # only with CMPI_BENCH_COLLECTIVES=1, so a multi-GPU scaling run cannot stall on them)
         colls = {"skipped": "multi-rank run without CMPI_BENCH_COLLECTIVES=1"}

@@ -147,6 +147,8 @@ struct HostPipe {
   hipEvent_t in_ready[4], k_done[4], slot_free[4];  // per staging slot (g_host_slots <= 4 in use)
   uint8_t* buf = nullptr;   // device staging, 2 slots
   uint8_t* hbuf = nullptr;  // pinned host staging, 2 slots (pageable user buffers)
+  uint8_t* dnon = nullptr;  // device: the whole batch's nonces, one H2D per call (page-locked nonces)
+  size_t dnon_cap = 0;
   size_t cap = 0;           // bytes per slot
   size_t ns = 0;            // slots allocated
   int32_t* hst = nullptr;   // pinned per-record open status of the whole batch
@@ -1079,7 +1081,11 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const size_t npitch = n_flat ? nonce_stride : 16;
   const size_t NS = (size_t)g_host_slots.load();  // staging slots (chunks in flight)
   const size_t per = std::max<size_t>(1, g_host_chunk.load() / std::max<size_t>(std::max(ip, op), 16));
-  const size_t K = std::min(per, nrec);  // records per chunk
+  // records per chunk: at most `per`, and the chunks of a batch equal — a short last chunk (e.g.
+  // 1 012 of 65 536 x 1 KiB after four of 16 131) took the FLOW plan, whose one-workgroup-per-CU
+  // kernel then waited for the CUs of the previous chunk's D2H, a blit kernel: 314 us for 1 MiB
+  // (rocprofv3 --kernel-trace --memory-copy-trace, profiles/r06e_hostpipe_timeline.txt)
+  const size_t K = (nrec + (nrec + per - 1) / per - 1) / ((nrec + per - 1) / per);
   // every region and slot 2 MiB aligned (DMA into regions that straddle 2 MiB boundaries ran
   // 20.6 instead of 33 GiB/s in some allocation histories, tools/host_calls.py)
   auto up2m = [](size_t x) { return (x + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1); };
@@ -1113,6 +1119,18 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
     P.cap = slot_b;
     P.ns = NS;
+  }
+  // page-locked nonces at a small stride: one H2D of the whole batch's nonces up front instead of
+  // one small copy per chunk on the H2D stream (each ~10 us of latency plus its gap in front of
+  // the next chunk's input copy, the stream that bounds the pipeline)
+  const bool n_once = n_flat && nrec > K;
+  if (n_once && P.dnon_cap < nrec * npitch) {
+    for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
+    if (P.dnon) (void)hipFree(P.dnon);
+    P.dnon = nullptr;
+    P.dnon_cap = 0;
+    if (hipMalloc(&P.dnon, nrec * npitch) != hipSuccess) return fail(CMPI_ENOMEM, "hipMalloc nonces failed");
+    P.dnon_cap = nrec * npitch;
   }
   if (DEC && P.hst_cap < nrec) {  // statuses land here by DMA, chunk by chunk
     for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
@@ -1182,7 +1200,9 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
       else
         HIP_TRY(hipMemcpyAsync(d.in, h.in, ip * nr, hipMemcpyHostToDevice, P.s[0]));
     }
-    if (n_flat)
+    if (n_once) {
+      if (ci == 0) HIP_TRY(hipMemcpyAsync(P.dnon, nonces, (nrec - 1) * npitch + 12, hipMemcpyHostToDevice, P.s[0]));
+    } else if (n_flat)
       HIP_TRY(hipMemcpyAsync(d.n, nonces + r0 * nonce_stride, (nr - 1) * npitch + 12, hipMemcpyHostToDevice, P.s[0]));
     else
       HIP_TRY(hipMemcpyAsync(d.n, h.n, 16 * nr, hipMemcpyHostToDevice, P.s[0]));
@@ -1190,10 +1210,11 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     HIP_TRY(hipEventRecord(P.in_ready[sl], P.s[0]));
     HIP_TRY(hipStreamWaitEvent(P.s[1], P.in_ready[sl], 0));
     void* wsp = ws_b ? (void*)d.ws : nullptr;
+    const uint8_t* dn = n_once ? P.dnon + r0 * npitch : d.n;
     if (OCB)
-      rc = ocb_batch<DEC>(c, d.out, op, d.in, ip, d.n, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
+      rc = ocb_batch<DEC>(c, d.out, op, d.in, ip, dn, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
     else
-      rc = gcm_batch<DEC>(c, d.out, op, d.in, ip, d.n, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
+      rc = gcm_batch<DEC>(c, d.out, op, d.in, ip, dn, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
     if (rc) break;
     if ((rc = step("kernel", ci))) break;
     HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
@@ -1430,6 +1451,7 @@ void cmpi_ctx_free(cmpi_ctx* c) {
       }
     }
     if (P.buf) (void)hipFree(P.buf);
+    if (P.dnon) (void)hipFree(P.dnon);
     if (P.hbuf) (void)hipHostFree(P.hbuf);
     if (P.hst) (void)hipHostFree(P.hst);
     if (P.dbounce) (void)hipHostFree(P.dbounce);
