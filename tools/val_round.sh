@@ -3,7 +3,8 @@
 # suite, smoke(), the default bench, the single-message latency table, then (PROF=1) the bench under
 # rocprofv3 --kernel-trace --stats: the default command, and the headline alone (--no-extras), whose
 # --stats average of the dominant kernel is the one the line's roofline uses.  Every step under its
-# own time limit; the first failure ends the pass.  Results in gpurun_out/${R}_*.
+# own time limit; the first failure ends the pass.  PMC=1 adds the config-2 counter passes
+# (tools/gpu_pmc.sh).  Results in gpurun_out/${R}_*.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -17,5 +18,8 @@ if [ -n "$PROF" ]; then
       python3 bench.py --no-extras > gpurun_out/${R}_headline_under_rocprof.json 2> gpurun_out/${R}_headline_under_rocprof.err || exit $?
   timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${R}_bench -o run -- \
       python3 bench.py > gpurun_out/${R}_bench_under_rocprof.json 2> gpurun_out/${R}_bench_under_rocprof.err || exit $?
+fi
+if [ -n "$PMC" ]; then  # counters of the config-2 seal / open (summarise here: LAST=5 tools/pmc_summarize.py)
+  WL=gcm1k PMC_OUT=gpurun_out/${R}_pmc_gcm1k timeout -k 10 400 bash tools/gpu_pmc.sh || exit $?
 fi
 echo VAL_DONE
