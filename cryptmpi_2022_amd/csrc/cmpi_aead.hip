@@ -254,6 +254,20 @@ int record_keys(const cmpi_ctx* c, hipStream_t stream) {
 // (tools/queue_probe.py, profiles/r04a_queue_probe.jsonl: a kernel on another stream waited up to
 // 98 ms behind the service at normal priority, <= 0.6 ms once its streams were warm at high).
 std::atomic<int> g_stream_mode{0};
+#ifndef CMPI_PIPE_H2D_LOW
+#define CMPI_PIPE_H2D_LOW 1
+#endif
+#ifndef CMPI_ASYNC_PRIO_SPLIT
+#define CMPI_ASYNC_PRIO_SPLIT 0
+#endif
+// A non-blocking library stream at the least priority (a pool of hardware queues apart from the
+// normal-priority streams of the caller, torch and the rest of the library)
+hipError_t low_stream(hipStream_t* s) {
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+}
 hipError_t lib_stream(hipStream_t* s, bool own_pool = false) {
   const int mode = own_pool ? 1 : g_stream_mode.load();
   if (mode == 1) {
@@ -1055,7 +1069,19 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   std::unique_lock<std::mutex> lk(c->hmu);  // the pipeline and its staging are per ctx
   HostPipe& P = *c->pipe;
   if (!P.init) {
-    for (auto& st : P.s) HIP_TRY(lib_stream(&st));
+    // The H2D stream at the least priority, in a pool of hardware queues of its own: HIP maps
+    // streams onto at most GPU_MAX_HW_QUEUES queues per priority, and when the H2D and the D2H
+    // stream landed on one queue (it depends on what streams the process made before — in
+    // round 6's bench sequence it did) each chunk's input copy waited for the previous chunk's D2H
+    // blit kernel: 24.5 instead of 34.3 GiB/s (profiles/r06j_*, r06k_*).  The kernel and D2H
+    // streams stay at normal priority (the greatest-priority pool holds the resident services).
+    for (int i = 0; i < 3; ++i) {
+      if (i == 0 && CMPI_PIPE_H2D_LOW) {
+        HIP_TRY(low_stream(&P.s[0]));
+      } else {
+        HIP_TRY(lib_stream(&P.s[i]));
+      }
+    }
     for (int i = 0; i < 4; ++i) {
       HIP_TRY(hipEventCreateWithFlags(&P.in_ready[i], kOrderEvent));
       HIP_TRY(hipEventCreateWithFlags(&P.k_done[i], kOrderEvent));

@@ -27,7 +27,8 @@
  * Prints one JSON line: one-way latency (round trip / 2) median / mean / p90 in us.  Each side
  * checks every received plaintext against what its peer sent (the message carries its index).
  * Both processes bind to the CPUs of the GPU's NUMA node (CMPI_NUMA_BIND=0: no binding).
- * PINGPONG_REGISTER_USER=1 page-locks the user buffers as well (attribution of the bounce copies).
+ * PINGPONG_REGISTER_USER=1 page-locks the user buffers as well (attribution of the bounce copies);
+ * PINGPONG_DUMP=<path> writes rank 1's last received wire record and its plaintext (parity tests).
  */
 #define _GNU_SOURCE
 #include <ctype.h>
@@ -253,6 +254,14 @@ static int run_side(int rank, int secure, size_t n, long iters, double warm_s, C
       }
     }
     if (rank == 0 && total >= 0 && i >= total - iters) rtt[i - (total - iters)] = now_us() - t0;
+    /* PINGPONG_DUMP=<path>: rank 1 writes the last wire record it received (nonce || ct || tag, as
+     * large_recv_buffer holds it) and the plaintext it opened, for a parity check against an oracle */
+    const char *dump = getenv("PINGPONG_DUMP");
+    if (dump && secure && rank == 1 && stop) {
+      FILE *f = fopen(dump, "wb");
+      if (!f || fwrite(large_recv_buffer, 1, n + 28, f) != n + 28 || fwrite(rbuf, 1, n, f) != n) bad = 1;
+      if (f) fclose(f);
+    }
     if ((rank == 0 && total >= 0 && i + 1 == total) || (rank == 1 && stop)) break;
   }
   if (rank == 0) fprintf(stderr, "numa_node=%d bound_cpus=%d\n", node, bound);
