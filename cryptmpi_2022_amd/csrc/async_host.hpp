@@ -68,8 +68,7 @@ int pool_stream(StagePool& P, hipStream_t* st) {
   if (P.streams.empty()) {
     for (size_t i = 0; i < kAsyncStreams; ++i) {
       hipStream_t s;
-      if (CMPI_ASYNC_PRIO_SPLIT && (i & 1u)) HIP_TRY(low_stream(&s));
-      else HIP_TRY(lib_stream(&s));
+      HIP_TRY(lib_stream(&s));
       P.streams.push_back(s);
     }
   }

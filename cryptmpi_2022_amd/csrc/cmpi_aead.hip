@@ -254,19 +254,15 @@ int record_keys(const cmpi_ctx* c, hipStream_t stream) {
 // (tools/queue_probe.py, profiles/r04a_queue_probe.jsonl: a kernel on another stream waited up to
 // 98 ms behind the service at normal priority, <= 0.6 ms once its streams were warm at high).
 std::atomic<int> g_stream_mode{0};
-#ifndef CMPI_PIPE_H2D_LOW
-#define CMPI_PIPE_H2D_LOW 1
-#endif
-#ifndef CMPI_ASYNC_PRIO_SPLIT
-#define CMPI_ASYNC_PRIO_SPLIT 0
-#endif
-// A non-blocking library stream at the least priority (a pool of hardware queues apart from the
-// normal-priority streams of the caller, torch and the rest of the library)
-hipError_t low_stream(hipStream_t* s) {
-  int least = 0, greatest = 0;
-  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+// A stream with a CU mask over every CU: a hardware queue of its own (blocking)
+hipError_t cu_stream(hipStream_t* s) {
+  int dev = 0, ncu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
-  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+  std::vector<uint32_t> m((size_t)(ncu + 31) / 32, ~0u);
+  if (ncu % 32) m.back() = (1u << (ncu % 32)) - 1u;
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)m.size(), m.data());
 }
 hipError_t lib_stream(hipStream_t* s, bool own_pool = false) {
   const int mode = own_pool ? 1 : g_stream_mode.load();
@@ -276,15 +272,7 @@ hipError_t lib_stream(hipStream_t* s, bool own_pool = false) {
     if (e != hipSuccess) return e;
     return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
   }
-  if (mode == 2) {
-    int dev = 0, ncu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    std::vector<uint32_t> m((size_t)(ncu + 31) / 32, ~0u);
-    if (ncu % 32) m.back() = (1u << (ncu % 32)) - 1u;
-    return hipExtStreamCreateWithCUMask(s, (uint32_t)m.size(), m.data());
-  }
+  if (mode == 2) return cu_stream(s);
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
@@ -1069,19 +1057,18 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   std::unique_lock<std::mutex> lk(c->hmu);  // the pipeline and its staging are per ctx
   HostPipe& P = *c->pipe;
   if (!P.init) {
-    // The H2D stream at the least priority, in a pool of hardware queues of its own: HIP maps
+    // The H2D stream on a hardware queue of its own (a CU-masked stream): HIP maps the other
     // streams onto at most GPU_MAX_HW_QUEUES queues per priority, and when the H2D and the D2H
-    // stream landed on one queue (it depends on what streams the process made before — in
-    // round 6's bench sequence it did) each chunk's input copy waited for the previous chunk's D2H
-    // blit kernel: 24.5 instead of 34.3 GiB/s (profiles/r06j_*, r06k_*).  The kernel and D2H
-    // streams stay at normal priority (the greatest-priority pool holds the resident services).
-    for (int i = 0; i < 3; ++i) {
-      if (i == 0 && CMPI_PIPE_H2D_LOW) {
-        HIP_TRY(low_stream(&P.s[0]));
-      } else {
-        HIP_TRY(lib_stream(&P.s[i]));
-      }
-    }
+    // stream landed on one queue (it depends on what streams the process made before — in round
+    // 6's bench sequence they did) each chunk's input copy waited for the previous chunk's D2H blit
+    // kernel: 24.5 GiB/s instead of 31.8-34.7 (profiles/r06jkmn_stream_queue_ab.jsonl: the H2D
+    // stream at the least priority instead gave 34.3-34.7 but cost the 602 outer-message requests
+    // on the normal-priority pool 20-25 %; every library stream at the greatest priority gave 34.3
+    // and kept them, but shares the resident services' queues).  A CU-masked stream is blocking: a host-path call also
+    // waits for work queued before it on the legacy null stream (it is synchronous anyway).
+    HIP_TRY(cu_stream(&P.s[0]));
+    HIP_TRY(lib_stream(&P.s[1]));
+    HIP_TRY(lib_stream(&P.s[2]));
     for (int i = 0; i < 4; ++i) {
       HIP_TRY(hipEventCreateWithFlags(&P.in_ready[i], kOrderEvent));
       HIP_TRY(hipEventCreateWithFlags(&P.k_done[i], kOrderEvent));
