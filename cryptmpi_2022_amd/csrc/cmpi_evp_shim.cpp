@@ -253,8 +253,16 @@ struct StaticSeg {
 struct StaticSegs {
   std::vector<StaticSeg*> v;
 };
-const size_t kRegStatic = env_size("CMPI_EVP_REGISTER_STATIC", 1);
-const size_t kRegStaticMax = env_size("CMPI_EVP_REGISTER_STATIC_MAX", (size_t)1 << 30);
+// (function-local statics: the snapshot below runs from a constructor, which may run before this
+// translation unit's namespace-scope initialisers)
+size_t reg_static_on() {
+  static const size_t v = env_size("CMPI_EVP_REGISTER_STATIC", 1);
+  return v;
+}
+size_t reg_static_max() {
+  static const size_t v = env_size("CMPI_EVP_REGISTER_STATIC_MAX", (size_t)1 << 30);
+  return v;
+}
 
 int collect_seg(struct dl_phdr_info* info, size_t, void* arg) {
   auto* segs = static_cast<StaticSegs*>(arg);
@@ -271,7 +279,7 @@ int collect_seg(struct dl_phdr_info* info, size_t, void* arg) {
     if (relro_end > a && relro_end < b) a = relro_end;
     // whole writable pages only: the first may share a page with the RELRO (read-only) part
     const uintptr_t lo = (a + pg - 1) & ~(pg - 1), hi = (b + pg - 1) & ~(pg - 1);
-    if (hi > lo && hi - lo <= kRegStaticMax) {
+    if (hi > lo && hi - lo <= reg_static_max()) {
       auto* s = new StaticSeg();
       s->lo = lo;
       s->hi = hi;
@@ -286,7 +294,7 @@ int collect_seg(struct dl_phdr_info* info, size_t, void* arg) {
 const StaticSegs& static_segs() {
   static const StaticSegs* s = [] {
     auto* x = new StaticSegs();
-    if (kRegStatic) dl_iterate_phdr(collect_seg, x);
+    if (reg_static_on()) dl_iterate_phdr(collect_seg, x);
     return x;
   }();
   return *s;
@@ -295,7 +303,7 @@ __attribute__((constructor)) void snapshot_static_segs() { (void)static_segs(); 
 
 // [p, p + n) inside a static segment: page-lock that segment (once; a failure leaves it pageable).
 void register_static(const void* p, size_t n) {
-  if (!kRegStatic || !p || n < 4096) return;  // small messages: the bounce copy is cheaper
+  if (!reg_static_on() || !p || n < 4096) return;  // small messages: the bounce copy is cheaper
   const uintptr_t a = (uintptr_t)p, b = a + n;
   for (StaticSeg* s : static_segs().v)
     if (a >= s->lo && b <= s->hi) {
