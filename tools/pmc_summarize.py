@@ -43,8 +43,9 @@ for k, cs in agg.items():
     avg = {c: sum(v) / len(v) for c, v in cs.items()}
     dur = sum(durs[k]) / len(durs[k])
     e = {"counters_avg": {c: round(v, 1) for c, v in avg.items()}, "avg_duration_us": round(dur * 1e6, 2)}
-    if "GRBM_GUI_ACTIVE" in avg:
-        e["clock_GHz"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9, 3)
+    if "GRBM_GUI_ACTIVE" in avg:  # GPU-busy cycles summed over the XCDs, as collected (no clock derived:
+        # the per-XCD division is not documented for gfx950 and gave clocks above the part's peak)
+        e["grbm_gui_active"] = avg["GRBM_GUI_ACTIVE"]
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         e["hbm_read_bytes"] = int(avg["FETCH_SIZE"] * 2 * 1024)
         e["hbm_write_bytes"] = int(avg["WRITE_SIZE"] * 1024)
