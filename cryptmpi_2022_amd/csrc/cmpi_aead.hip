@@ -1066,7 +1066,13 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     // on the normal-priority pool 20-25 %; every library stream at the greatest priority gave 34.3
     // and kept them, but shares the resident services' queues).  A CU-masked stream is blocking: a host-path call also
     // waits for work queued before it on the legacy null stream (it is synchronous anyway).
-    HIP_TRY(cu_stream(&P.s[0]));
+    // (the hardware has a finite number of queues: when a dedicated one cannot be had, an ordinary
+    // library stream still works, only without the guarantee)
+    const hipError_t prior = hipPeekAtLastError();
+    if (cu_stream(&P.s[0]) != hipSuccess) {
+      if (prior == hipSuccess) (void)hipGetLastError();  // clear our own error, never the caller's
+      HIP_TRY(lib_stream(&P.s[0]));
+    }
     HIP_TRY(lib_stream(&P.s[1]));
     HIP_TRY(lib_stream(&P.s[2]));
     for (int i = 0; i < 4; ++i) {
