@@ -131,6 +131,7 @@ _SIGS = {
     "cmpi_debug_set_ctr_wg_per_cu": ([_I], None),
     "cmpi_debug_set_lane_pair": ([_I], None),
     "cmpi_debug_set_svc_ls_min": ([_I], None),
+    "cmpi_debug_set_svc_fake_stuck": ([_I], None),
     "cmpi_debug_set_flow_one_wg": ([_I], None),
     "cmpi_debug_set_host_direct": ([_S], None),
     "cmpi_debug_set_host_spin": ([_I], None),

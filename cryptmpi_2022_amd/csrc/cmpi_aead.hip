@@ -1512,6 +1512,7 @@ void cmpi_debug_set_host_spin(int mode) { g_host_spin.store(mode >= 0 && mode <=
 
 void cmpi_debug_set_flow_one_wg(int on) { g_flow_one_wg.store(on ? 1 : 0); }
 void cmpi_debug_set_svc_ls_min(int ls) { g_svc_ls_min.store(ls >= 0 && ls <= 3 ? ls : 0); }
+void cmpi_debug_set_svc_fake_stuck(int on) { g_svc_fake_stuck.store(on ? 1 : 0); }
 void cmpi_debug_set_lane_pair(int on) { g_lane_pair.store(on >= 1 && on <= 4 ? on : 0); }
 void cmpi_debug_set_flow_threads(int threads) { g_flow_nt.store(threads == 512 || threads == 1024 ? threads : 0); }
 void cmpi_debug_set_ctr_wg_per_cu(int n) { g_ctr_wg_per_cu.store(n >= 1 && n <= 2 ? n : 2); }

@@ -37,6 +37,9 @@ SvcSlot& svc_slot(int dev, int i) {
 }
 std::atomic<uint32_t> g_svc_next_slot[kSvcMaxDevices];
 std::atomic<int> g_svc_ls_min{0};  // cmpi_debug_set_svc_ls_min (A/B of the service's chunk length)
+// cmpi_debug_set_svc_fake_stuck (test): the next shutdowns treat the stop as failed and the
+// generation as still resident, exercising the path that leaks the Svc
+std::atomic<int> g_svc_fake_stuck{0};
 
 struct Svc {
   hipStream_t st = nullptr;    // the slot's stream (shared; not owned)
@@ -242,10 +245,11 @@ int svc_stop_locked(Svc& S) {
 int svc_shutdown_locked(cmpi_ctx* c) {
   if (!c->svc) return CMPI_OK;
   Svc& S = *c->svc;
-  const int rc = svc_stop_locked(S);
-  bool gone = !rc || !S.launched || svc_exited(S);
+  const bool fake = g_svc_fake_stuck.load() != 0;
+  const int rc = fake ? fail(CMPI_EHIP, "message service stop failed (test hook)") : svc_stop_locked(S);
+  bool gone = !fake && (!rc || !S.launched || svc_exited(S));
   for (const auto t0 = std::chrono::steady_clock::now();
-       !gone && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200);)
+       !fake && !gone && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200);)
     gone = svc_exited(S);
   if (gone) {
     svc_release(S);  // clears every slot that names it

@@ -57,6 +57,10 @@ void cmpi_debug_set_lane_pair(int on);
 /* resident service: smallest chunk length exponent (chunks of 64·2^ls blocks, 0..3; 0 default),
  * taken at the service's next launch. */
 void cmpi_debug_set_svc_ls_min(int ls);
+/* Test hook: service shutdowns (cmpi_service_stop, re-key, cmpi_ctx_free) treat the stop as failed
+ * and the generation as still resident, so the service object is leaked, never freed while a stream
+ * slot may still name it (1 on, 0 off). */
+void cmpi_debug_set_svc_fake_stuck(int on);
 /* FLOW kernel: a batch whose chunks all fit one workgroup finishes its tags in-kernel (1, default)
  * or through the XOR-combine launch (0). */
 void cmpi_debug_set_flow_one_wg(int on);

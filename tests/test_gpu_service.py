@@ -175,6 +175,39 @@ def test_service_many_contexts_share_slots():
     assert max(lat[6:]) < 0.05, [round(v * 1e3, 2) for v in lat]
 
 
+def test_service_stuck_shutdown_then_new_services():
+    """A shutdown whose stop fails with the generation still resident (forced by the test hook
+    cmpi_debug_set_svc_fake_stuck) leaks the service object instead of freeing it, because a stream
+    slot still names it as its owner (svc_launch reads the owner's exit word and writes
+    its kick word).  Services started afterwards on other contexts — taking every slot, the
+    stuck one's included — serve bit-exact messages."""
+    ctx = aead.AeadCtx(KEY)
+    ctx.service_start(2000)
+    pt = splitmix64_bytes(0x57, 5000).tobytes()
+    nonce = splitmix64_bytes(0x58, 12).tobytes()
+    assert ctx.seal(nonce, pt) == oracle.gcm_seal(KEY, nonce, pt)
+    assert ctx.service_running()
+    N.lib().cmpi_debug_set_svc_fake_stuck(1)
+    try:
+        ctx.close()  # shutdown "fails": the Svc is leaked, its kernel idles out by itself
+    finally:
+        N.lib().cmpi_debug_set_svc_fake_stuck(0)
+    keys = [bytes([0x40 + k] * 16) for k in range(6)]
+    ctxs = [aead.AeadCtx(k) for k in keys]
+    for c in ctxs:
+        c.service_start(500000)
+    for i in range(24):
+        k = i % 6
+        p = splitmix64_bytes(0x600 + i, 777 + 13 * i).tobytes()
+        nn = splitmix64_bytes(0x700 + i, 12).tobytes()
+        got = ctxs[k].seal(nn, p)
+        assert got == oracle.gcm_seal(keys[k], nn, p), i
+        assert ctxs[k].open(nn, got) == p
+    for c in ctxs:
+        c.service_stop()
+        c.close()
+
+
 def test_service_many_contexts_two_threads():
     """Two host threads, each round-robin over three of six serviced contexts (4 stream slots):
     launches on held slots kick other threads' generations while their messages are posted; every
