@@ -134,6 +134,7 @@ _SIGS = {
     "cmpi_debug_set_svc_fake_stuck": ([_I], None),
     "cmpi_debug_set_flow_one_wg": ([_I], None),
     "cmpi_debug_set_host_direct": ([_S], None),
+    "cmpi_debug_set_host_out_direct": ([_I], None),
     "cmpi_debug_set_host_spin": ([_I], None),
     "cmpi_debug_event_new": ([], _P),
     "cmpi_debug_copy": ([_P, _P, _S, _P], _I),

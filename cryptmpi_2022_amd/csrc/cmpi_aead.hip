@@ -39,6 +39,7 @@
 #include "gf128_host.hpp"
 #include "keysetup_kernels.hpp"
 #include "ocb_kernels.hpp"
+#include "hsa_copy.hpp"
 
 using cmpi::Blk;
 using cmpi::dev::u32x4;
@@ -158,6 +159,9 @@ struct HostPipe {
   uint32_t* hflag = nullptr;  // pinned coherent word: the direct path's completion sequence number
   uint32_t* dflag = nullptr;  // its device address
   uint32_t seq = 0;
+  hsa_signal_t dsig[4] = {};  // output modes 4-5: completion of each slot's SDMA D2H (value 0 = done)
+  hsa_signal_t hsig[4] = {};  // output mode 5: completion of each slot's SDMA H2D (records + nonces)
+  bool dsig_init = false;
   bool init = false;
 };
 
@@ -865,7 +869,23 @@ int ocb_batch(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
 // chunk i is reused by chunk i+NS once D2H(i) completed.  Pinned host buffers (hipHostMalloc /
 // cmpi_host_register) move by DMA at PCIe rate; pageable ones are staged by the HIP runtime.
 std::atomic<size_t> g_host_slots{3};  // staging slots, 2..4 (cmpi_debug_set_host_slots)
-std::atomic<size_t> g_host_chunk{(size_t)16 << 20};  // 8 / 16 / 32 MiB: 30.1 / 31.2 / 30.6 GiB/s pinned (tools/host_sweep.py)
+// 0 = automatic: 8 MiB when records, outputs and nonces are all page-locked (mode 5: 4 / 8 / 16 MiB
+// ran 37.3-37.6 / 37.2-37.5 / 35.6-36.1 GiB/s, tools/host_pipe_sweep.py r06ak), else 16 MiB (the
+// pageable path packs each chunk on the CPU: 8 MiB chunks ran it at 15.2 instead of 18-20)
+std::atomic<size_t> g_host_chunk{0};
+// Host pipeline copy modes (cmpi_debug_set_host_out_direct), page-locked dense outputs:
+//   0  hipMemcpyAsync both ways (HIP runs a D2H into page-locked memory as a blit kernel, and
+//      while one runs no other command of the pipeline starts: kernel and D2H of each chunk in
+//      series, 34.8 GiB/s — profiles/r06_hostpath_timelines.txt);
+//   1  the kernel writes the outputs (and open's statuses) over PCIe itself (32.9: the kernel's
+//      scattered 16-byte stores reach 49 GB/s where a copy reaches 57);
+//   4  hipMemcpyAsync H2D, D2H on an SDMA engine through HSA (hsa_copy.hpp), issued by this thread
+//      when the chunk's kernel is done (37.0);
+//   5  both ways on SDMA through HSA, this thread launching each chunk's kernel when its input
+//      landed — no HIP event between copies and kernels (the marker after each H2D held the next
+//      H2D and the kernel ~23 us) (37.4) — needs page-locked inputs, outputs and nonces and more
+//      than one chunk; otherwise mode 4's D2H, otherwise mode 0.
+std::atomic<int> g_host_out_direct{5};
 
 // true when p lies in page-locked host memory (hipHostMalloc / hipHostRegister): it can be the
 // direct source/target of an asynchronous DMA.  Pageable memory is never handed to async copies
@@ -1099,7 +1119,9 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const bool n_flat = (nrec == 1 || nonce_stride <= 64) && is_pinned(nonces);
   const size_t npitch = n_flat ? nonce_stride : 16;
   const size_t NS = (size_t)g_host_slots.load();  // staging slots (chunks in flight)
-  const size_t per = std::max<size_t>(1, g_host_chunk.load() / std::max<size_t>(std::max(ip, op), 16));
+  size_t chunk_b = g_host_chunk.load();
+  if (!chunk_b) chunk_b = in_flat && out_flat && n_flat ? ((size_t)8 << 20) : ((size_t)16 << 20);
+  const size_t per = std::max<size_t>(1, chunk_b / std::max<size_t>(std::max(ip, op), 16));
   // records per chunk: at most `per`, and the chunks of a batch equal — a short last chunk (e.g.
   // 1 012 of 65 536 x 1 KiB after four of 16 131) took the FLOW plan, whose one-workgroup-per-CU
   // kernel then waited for the CUs of the previous chunk's D2H, a blit kernel: 314 us for 1 MiB
@@ -1167,6 +1189,12 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const bool cpu_pack = (in_rec && !in_pinned) || !n_flat;
   const bool cpu_unpack = out_rec && !out_pinned;
   const size_t nchunks = (nrec + K - 1) / K;
+  // the device addresses of the caller's page-locked outputs (and of the status array) for the
+  // copy modes that write them without hipMemcpyAsync (g_host_out_direct)
+  const int omode = g_host_out_direct.load();
+  uint8_t* dout_all = out_rec && out_flat && omode ? (uint8_t*)pinned_dev_ptr(out) : nullptr;
+  int32_t* dst_all = DEC && dout_all ? (int32_t*)pinned_dev_ptr(P.hst) : nullptr;
+  if (DEC && !dst_all) dout_all = nullptr;
   static const bool dbg_sync = getenv("CMPI_DEBUG_SYNC") != nullptr;  // diagnose: sync + check each step
   auto step = [&](const char* what, size_t ci) -> int {
     if (!dbg_sync) return CMPI_OK;
@@ -1198,7 +1226,138 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     par_copy_records(out + r0 * out_stride, out_stride, h.out, op, out_rec, nr);
     return CMPI_OK;
   };
+  // modes 4-5: D2H on an SDMA engine through HSA, issued by this thread once the chunk's kernel is
+  // done; a slot is reused after its copy's signal reached 0
+  const HsaAgents* ha = nullptr;
+  uint8_t* sd_out = nullptr;
+  int32_t* sd_st = nullptr;
+  if (omode >= 4 && dout_all) {
+    const HsaAgents& a = hsa_agents(c->device);
+    if (a.ok) {
+      if (!P.dsig_init) {
+        for (int i = 0; i < 8; ++i)
+          if (hsa_signal_create(0, 0, nullptr, i < 4 ? &P.dsig[i] : &P.hsig[i - 4]) != HSA_STATUS_SUCCESS) {
+            for (int j = 0; j < i; ++j) (void)hsa_signal_destroy(j < 4 ? P.dsig[j] : P.hsig[j - 4]);
+            return fail(CMPI_EHIP, "hsa_signal_create failed");
+          }
+        P.dsig_init = true;
+      }
+      ha = &a;
+      sd_out = dout_all;
+      sd_st = dst_all;
+    }
+  }
+  if (omode != 1) dout_all = nullptr, dst_all = nullptr;  // mode 1 alone: the kernel writes them
+  auto sdma_wait = [&](int sl) {
+    (void)hsa_signal_wait_scacquire(P.dsig[sl], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+  };
+  // D2H of chunk ci by SDMA: wait (spinning) for its kernel, then one copy (+ the statuses)
+  auto sdma_d2h = [&](size_t ci) -> int {
+    const int sl = (int)(ci % NS);
+    const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
+    const auto d = layout(sl, P.buf);
+    hipError_t q;
+    while ((q = hipEventQuery(P.k_done[sl])) == hipErrorNotReady) {
+    }
+    if (q != hipSuccess) return fail(CMPI_EHIP, "chunk %zu kernel: %s", ci, hipGetErrorString(q));
+    hsa_signal_store_relaxed(P.dsig[sl], DEC ? 2 : 1);
+    if (sdma_copy(sd_out + r0 * out_stride, ha->cpu, d.out, ha->gpu, (nr - 1) * op + out_rec, 0, nullptr, P.dsig[sl],
+                  ha->eng_d2h) != HSA_STATUS_SUCCESS) {
+      hsa_signal_store_relaxed(P.dsig[sl], 0);  // nothing in flight on this slot
+      return fail(CMPI_EHIP, "hsa_amd_memory_async_copy (chunk %zu) failed", ci);
+    }
+    if (DEC && sdma_copy(sd_st + r0, ha->cpu, d.st, ha->gpu, 4 * nr, 0, nullptr, P.dsig[sl], ha->eng_d2h) != HSA_STATUS_SUCCESS) {
+      hsa_signal_subtract_relaxed(P.dsig[sl], 1);  // only the record copy is in flight
+      return fail(CMPI_EHIP, "hsa_amd_memory_async_copy (chunk %zu statuses) failed", ci);
+    }
+    return CMPI_OK;
+  };
+  // mode 5: both directions on SDMA engines through HSA, the host launching each chunk's kernel
+  // when its input copy's signal reached 0 — no HIP event between the copies and the kernels (the
+  // marker after each input copy held both the next copy and the kernel ~23 us, r06ag)
+  uint8_t* in_d = ha && omode == 5 && in_flat && n_once ? (uint8_t*)pinned_dev_ptr(in) : nullptr;
+  uint8_t* non_d = in_d ? (uint8_t*)pinned_dev_ptr(nonces) : nullptr;
+  if (in_d && non_d) {
+    auto sig_ok = [&](hsa_signal_t sg) {
+      return hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) == 0;
+    };
+    auto issue_in = [&](size_t ci) -> int {
+      const int sl = (int)(ci % NS);
+      const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
+      const auto d = layout(sl, P.buf);
+      const uint32_t ndep = ci >= NS ? 1u : 0u;  // chunk ci-NS's output copy has read the slot
+      hsa_signal_store_relaxed(P.hsig[sl], ci == 0 ? 2 : 1);
+      if (ci == 0 && sdma_copy(P.dnon, ha->gpu, non_d, ha->cpu, (nrec - 1) * npitch + 12, 0, nullptr, P.hsig[sl],
+                               ha->eng_h2d) != HSA_STATUS_SUCCESS) {
+        hsa_signal_store_relaxed(P.hsig[sl], 0);
+        return fail(CMPI_EHIP, "hsa_amd_memory_async_copy (nonces) failed");
+      }
+      if (sdma_copy(d.in, ha->gpu, in_d + r0 * in_stride, ha->cpu, (nr - 1) * ip + in_rec, ndep, ndep ? &P.dsig[sl] : nullptr,
+                    P.hsig[sl], ha->eng_h2d) != HSA_STATUS_SUCCESS) {
+        hsa_signal_subtract_relaxed(P.hsig[sl], 1);
+        return fail(CMPI_EHIP, "hsa_amd_memory_async_copy (chunk %zu input) failed", ci);
+      }
+      return CMPI_OK;
+    };
+    int rc = CMPI_OK;
+    size_t ni = 0;  // chunks whose input copy has been issued
+    for (; ni < std::min(NS, nchunks) && !rc; ++ni) rc = issue_in(ni);
+    // one polling loop over both events that move the pipeline: a chunk's input landed (launch
+    // its kernel) and a chunk's kernel finished (its output copy, then the input copy of the chunk
+    // that takes the slot next, behind that output copy on the device)
+    size_t kl = 0, dl = 0;  // next kernel to launch, next output copy to issue
+    while (dl < nchunks && !rc) {
+      if (kl < ni) {
+        const int sl = (int)(kl % NS);
+        const hsa_signal_value_t v = hsa_signal_load_scacquire(P.hsig[sl]);
+        if (v < 0) {
+          rc = fail(CMPI_EHIP, "chunk %zu input copy failed (signal %ld)", kl, (long)v);
+          break;
+        }
+        if (v == 0) {
+          const size_t r0 = kl * K, nr = std::min(K, nrec - r0);
+          const auto d = layout(sl, P.buf);
+          void* wsp = ws_b ? (void*)d.ws : nullptr;
+          rc = OCB ? ocb_batch<DEC>(c, d.out, op, d.in, ip, P.dnon + r0 * npitch, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1])
+                   : gcm_batch<DEC>(c, d.out, op, d.in, ip, P.dnon + r0 * npitch, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
+          if (rc) break;
+          HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
+          ++kl;
+        }
+      }
+      if (dl < kl) {
+        const hipError_t q = hipEventQuery(P.k_done[dl % NS]);
+        if (q == hipSuccess) {
+          if ((rc = sdma_d2h(dl))) break;
+          if (dl + NS < nchunks) {
+            if ((rc = issue_in(dl + NS))) break;
+            ++ni;
+          }
+          ++dl;
+        } else if (q != hipErrorNotReady) {
+          rc = fail(CMPI_EHIP, "chunk %zu kernel: %s", dl, hipGetErrorString(q));
+        }
+      }
+    }
+    for (size_t i = 0; i < NS; ++i) {  // nothing of this call in flight on return (also after an error)
+      if (!sig_ok(P.hsig[i]) && !rc) rc = fail(CMPI_EHIP, "input copy failed");
+      if (!sig_ok(P.dsig[i]) && !rc) rc = fail(CMPI_EHIP, "output copy failed");
+    }
+    HIP_TRY(hipStreamSynchronize(P.s[1]));
+    if (rc) return rc;
+    if (DEC) {
+      size_t bad = 0;
+      for (size_t i = 0; i < nrec; ++i) bad += P.hst[i] == 0;
+      if (status) memcpy(status, P.hst, 4 * nrec);
+      if (bad) return fail(CMPI_EAUTH, "%zu of %zu records failed authentication", bad, nrec);
+    }
+    return CMPI_OK;
+  }
   int rc = CMPI_OK;
+  // (Measured and not taken, round 6: the H2D on the kernel's stream, 33.0 GiB/s; the D2H on it,
+  // 30.6; all on one, 21.9; each stream on a hardware queue of its own, or the D2H confined to 16
+  // CUs beside the kernel: unchanged — the blit D2H still held the next kernel.)
+  hipStream_t sH = P.s[0], sK = P.s[1], sD = P.s[2];
   for (size_t ci = 0; ci < nchunks && !rc; ++ci) {
     const int sl = (int)(ci % NS);
     const size_t r0 = ci * K, nr = std::min(K, nrec - r0);
@@ -1210,46 +1369,65 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     if (in_rec && !in_pinned) par_copy_records(h.in, ip, in + r0 * in_stride, in_stride, in_rec, nr);
     if (!n_flat)
       for (size_t i = 0; i < nr; ++i) memcpy(h.n + 16 * i, nonces + (r0 + i) * nonce_stride, 12);
-    if (ci >= NS) HIP_TRY(hipStreamWaitEvent(P.s[0], P.slot_free[sl], 0));
+    if (ci >= NS && ha)
+      sdma_wait(sl);  // chunk ci-NS's SDMA copy has read the slot
+    else if (ci >= NS)
+      HIP_TRY(hipStreamWaitEvent(sH, P.slot_free[sl], 0));
+    // the batch's nonces ahead of chunk 0's records: the first kernel then starts when they land
+    if (n_once && ci == 0) HIP_TRY(hipMemcpyAsync(P.dnon, nonces, (nrec - 1) * npitch + 12, hipMemcpyHostToDevice, sH));
     if (in_rec) {
       if (in_flat)
-        HIP_TRY(hipMemcpyAsync(d.in, in + r0 * in_stride, (nr - 1) * ip + in_rec, hipMemcpyHostToDevice, P.s[0]));
+        HIP_TRY(hipMemcpyAsync(d.in, in + r0 * in_stride, (nr - 1) * ip + in_rec, hipMemcpyHostToDevice, sH));
       else if (in_pinned)
-        HIP_TRY(hipMemcpy2DAsync(d.in, ip, in + r0 * in_stride, in_stride, in_rec, nr, hipMemcpyHostToDevice, P.s[0]));
+        HIP_TRY(hipMemcpy2DAsync(d.in, ip, in + r0 * in_stride, in_stride, in_rec, nr, hipMemcpyHostToDevice, sH));
       else
-        HIP_TRY(hipMemcpyAsync(d.in, h.in, ip * nr, hipMemcpyHostToDevice, P.s[0]));
+        HIP_TRY(hipMemcpyAsync(d.in, h.in, ip * nr, hipMemcpyHostToDevice, sH));
     }
     if (n_once) {
-      if (ci == 0) HIP_TRY(hipMemcpyAsync(P.dnon, nonces, (nrec - 1) * npitch + 12, hipMemcpyHostToDevice, P.s[0]));
     } else if (n_flat)
-      HIP_TRY(hipMemcpyAsync(d.n, nonces + r0 * nonce_stride, (nr - 1) * npitch + 12, hipMemcpyHostToDevice, P.s[0]));
+      HIP_TRY(hipMemcpyAsync(d.n, nonces + r0 * nonce_stride, (nr - 1) * npitch + 12, hipMemcpyHostToDevice, sH));
     else
-      HIP_TRY(hipMemcpyAsync(d.n, h.n, 16 * nr, hipMemcpyHostToDevice, P.s[0]));
+      HIP_TRY(hipMemcpyAsync(d.n, h.n, 16 * nr, hipMemcpyHostToDevice, sH));
     if ((rc = step("H2D", ci))) break;
-    HIP_TRY(hipEventRecord(P.in_ready[sl], P.s[0]));
-    HIP_TRY(hipStreamWaitEvent(P.s[1], P.in_ready[sl], 0));
+    HIP_TRY(hipEventRecord(P.in_ready[sl], sH));
+    HIP_TRY(hipStreamWaitEvent(sK, P.in_ready[sl], 0));
     void* wsp = ws_b ? (void*)d.ws : nullptr;
     const uint8_t* dn = n_once ? P.dnon + r0 * npitch : d.n;
+    uint8_t* ko = dout_all ? dout_all + r0 * out_stride : d.out;
+    int32_t* ks = DEC ? (dout_all ? dst_all + r0 : d.st) : nullptr;
     if (OCB)
-      rc = ocb_batch<DEC>(c, d.out, op, d.in, ip, dn, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
+      rc = ocb_batch<DEC>(c, ko, op, d.in, ip, dn, npitch, len, nr, ks, wsp, sK);
     else
-      rc = gcm_batch<DEC>(c, d.out, op, d.in, ip, dn, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
+      rc = gcm_batch<DEC>(c, ko, op, d.in, ip, dn, npitch, len, nr, ks, wsp, sK);
     if (rc) break;
     if ((rc = step("kernel", ci))) break;
-    HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
-    HIP_TRY(hipStreamWaitEvent(P.s[2], P.k_done[sl], 0));
+    if (dout_all) {  // nothing to copy back: the slot is free once the kernel has read it
+      HIP_TRY(hipEventRecord(P.slot_free[sl], sK));
+      continue;
+    }
+    HIP_TRY(hipEventRecord(P.k_done[sl], sK));
+    if (ha) {  // the previous chunk's output by SDMA (its kernel ran while this chunk's input copied)
+      if (ci >= 1 && (rc = sdma_d2h(ci - 1))) break;
+      continue;
+    }
+    HIP_TRY(hipStreamWaitEvent(sD, P.k_done[sl], 0));
     if (out_rec) {
       if (out_flat)
-        HIP_TRY(hipMemcpyAsync(out + r0 * out_stride, d.out, (nr - 1) * op + out_rec, hipMemcpyDeviceToHost, P.s[2]));
+        HIP_TRY(hipMemcpyAsync(out + r0 * out_stride, d.out, (nr - 1) * op + out_rec, hipMemcpyDeviceToHost, sD));
       else if (out_pinned)
-        HIP_TRY(hipMemcpy2DAsync(out + r0 * out_stride, out_stride, d.out, op, out_rec, nr, hipMemcpyDeviceToHost, P.s[2]));
+        HIP_TRY(hipMemcpy2DAsync(out + r0 * out_stride, out_stride, d.out, op, out_rec, nr, hipMemcpyDeviceToHost, sD));
       else
-        HIP_TRY(hipMemcpyAsync(h.out, d.out, op * nr, hipMemcpyDeviceToHost, P.s[2]));
+        HIP_TRY(hipMemcpyAsync(h.out, d.out, op * nr, hipMemcpyDeviceToHost, sD));
     }
-    if (DEC) HIP_TRY(hipMemcpyAsync(P.hst + r0, d.st, 4 * nr, hipMemcpyDeviceToHost, P.s[2]));
+    if (DEC)
+      HIP_TRY(hipMemcpyAsync(P.hst + r0, d.st, 4 * nr, hipMemcpyDeviceToHost, sD));
     if ((rc = step("D2H", ci))) break;
-    HIP_TRY(hipEventRecord(P.slot_free[sl], P.s[2]));
+    HIP_TRY(hipEventRecord(P.slot_free[sl], sD));
     if (cpu_unpack && ci >= 1 && (rc = unpack(ci - 1))) break;  // overlaps the GPU work of chunk ci
+  }
+  if (ha) {
+    if (!rc) rc = sdma_d2h(nchunks - 1);
+    for (size_t i = 0; i < NS; ++i) sdma_wait((int)i);  // every issued copy done (also after an error)
   }
   if (!rc && cpu_unpack) rc = unpack(nchunks - 1);
   for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
@@ -1475,6 +1653,10 @@ void cmpi_ctx_free(cmpi_ctx* c) {
     if (P.hst) (void)hipHostFree(P.hst);
     if (P.dbounce) (void)hipHostFree(P.dbounce);
     if (P.hflag) (void)hipHostFree(P.hflag);
+    if (P.dsig_init) {
+      for (auto& sg : P.dsig) (void)hsa_signal_destroy(sg);
+      for (auto& sg : P.hsig) (void)hsa_signal_destroy(sg);
+    }
   }
   if (c->dt) (void)hipFree(c->dt);
   memset(c->key, 0, 16);
@@ -1498,7 +1680,7 @@ int cmpi_host_unregister(void* ptr) {
   return CMPI_OK;
 }
 
-void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes ? bytes : ((size_t)16 << 20)); }
+void cmpi_debug_set_host_chunk(size_t bytes) { g_host_chunk.store(bytes); }
 
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
   g_force_L.store(lanes_per_record == 1 || lanes_per_record == 2 || lanes_per_record == 4 ? lanes_per_record : 0);
@@ -1506,6 +1688,7 @@ void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments) {
 }
 
 void cmpi_debug_set_host_direct(size_t bytes) { g_host_direct.store(bytes); }
+void cmpi_debug_set_host_out_direct(int mode) { g_host_out_direct.store(mode == 0 || mode == 1 || mode == 4 || mode == 5 ? mode : 5); }
 void cmpi_debug_set_host_slots(int slots) { g_host_slots.store(slots >= 2 && slots <= 4 ? (size_t)slots : 3); }
 void cmpi_debug_set_stream_mode(int mode) { g_stream_mode.store(mode >= 0 && mode <= 2 ? mode : 0); }
 void cmpi_debug_set_host_spin(int mode) { g_host_spin.store(mode >= 0 && mode <= 3 ? mode : 0); }

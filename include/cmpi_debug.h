@@ -19,7 +19,8 @@ extern "C" {
 /* Force GCM lanes-per-record (1, 2 or 4; anything else = automatic) and segments per record
  * (0 = automatic) for every subsequent launch in the process. */
 void cmpi_debug_force_plan(int lanes_per_record, uint32_t segments);
-/* Chunk bytes of the pipelined host path (*_host calls; 0 = default 16 MiB). */
+/* Chunk bytes of the pipelined host path (*_host calls; 0 = automatic: 8 MiB when records,
+ * outputs and nonces are page-locked, else 16 MiB). */
 void cmpi_debug_set_host_chunk(size_t bytes);
 /* Staging slots (chunks in flight) of the pipelined host path: 2..4, anything else = default 3. */
 void cmpi_debug_set_host_slots(int slots);
@@ -67,6 +68,14 @@ void cmpi_debug_set_flow_one_wg(int on);
 /* Host-memory calls (cmpi_*_host) up to `bytes` of input + output records run the direct path
  * (kernel on page-locked host memory, no DMA); larger ones the 3-stream pipeline.  0 = never. */
 void cmpi_debug_set_host_direct(size_t bytes);
+/* Host pipeline (cmpi_gcm/ocb_*_host, batches above the direct threshold), how chunks move:
+ * 0 = hipMemcpyAsync both ways; 1 = the kernel writes page-locked dense outputs (and open's
+ * statuses) over PCIe itself; 4 = hipMemcpyAsync H2D, D2H on an SDMA engine through HSA;
+ * 5 (default) = both directions on SDMA through HSA, the calling thread launching each chunk's
+ * kernel when its input landed (page-locked records, outputs and nonces, more than one chunk;
+ * otherwise mode 4's D2H where the outputs allow, otherwise mode 0).  Anything else = 5.
+ * Process-wide. */
+void cmpi_debug_set_host_out_direct(int mode);
 /* Direct host path: how the host waits for a call's kernels — 0 blocking hipStreamSynchronize,
  * 1 spin on a host word written by hipStreamWriteValue32, 2 the same word written by a one-wave
  * kernel, 3 polling hipStreamQuery. */

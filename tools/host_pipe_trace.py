@@ -6,6 +6,8 @@ timeline's summary: run it under rocprofv3, then `host_pipe_trace.py --summarize
     rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d D -o run -- python3 tools/host_pipe_trace.py
     python3 tools/host_pipe_trace.py --summarize D
 
+(CHUNK_MIB / OUT_DIRECT in the environment: the pipeline's chunk size and kernel-written outputs.)
+
 The summary takes the last call: per chunk the H2D copy, kernel and D2H copy intervals (us from
 the call's first copy), and the totals: the call's span, each engine's busy time, and the time
 when both directions copied at once."""
@@ -35,6 +37,9 @@ def run(calls: int = 6) -> None:
     out = bench.registered_host_buffer(nrec * (n + 16))
     ctx = aead.AeadCtx(bench.KEY, device=0)
     L, h = N.lib(), ctx.handle
+    if os.environ.get("CHUNK_MIB"):  # pipeline settings under test (cmpi_debug_set_host_chunk / _out_direct)
+        L.cmpi_debug_set_host_chunk(int(os.environ["CHUNK_MIB"]) << 20)
+    L.cmpi_debug_set_host_out_direct(int(os.environ.get("OUT_DIRECT", "0")))
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     rates = []
     for _ in range(calls):
@@ -50,7 +55,9 @@ def summarize(d: str) -> None:
         return list(csv.DictReader(open(f[0]))) if f else []
 
     cp = rows("*memory_copy_trace.csv")
-    kt = [r for r in rows("*kernel_trace.csv") if "cmpi::dev" in r["Kernel_Name"]]
+    # the library's kernels, and HIP's blit kernels (a D2H copy into page-locked memory runs as
+    # __amd_rocclr_copyBuffer, not on a copy engine)
+    kt = [r for r in rows("*kernel_trace.csv") if "cmpi::dev" in r["Kernel_Name"] or "__amd_rocclr_copyBuffer" in r["Kernel_Name"]]
     ev = [("copy", r.get("Direction", r.get("Operation", "?")), int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
            int(r.get("Bytes", r.get("Size", 0)) or 0)) for r in cp]
     ev += [("kernel", r["Kernel_Name"].split("(")[0].replace("void cmpi::dev::", ""), int(r["Start_Timestamp"]),
@@ -80,8 +87,8 @@ def summarize(d: str) -> None:
         return (tot + (cur[1] - cur[0] if cur else 0)) / 1e3, iv
 
     h2d, iv_h = busy(lambda k, w: k == "copy" and "HOST_TO_DEVICE" in w.upper())
-    d2h, iv_d = busy(lambda k, w: k == "copy" and "DEVICE_TO_HOST" in w.upper())
-    kern, _ = busy(lambda k, w: k == "kernel")
+    d2h, iv_d = busy(lambda k, w: (k == "copy" and "DEVICE_TO_HOST" in w.upper()) or "__amd_rocclr" in w)
+    kern, _ = busy(lambda k, w: k == "kernel" and "__amd_rocclr" not in w)
     both = 0
     for s1, e1 in iv_h:
         for s2, e2 in iv_d:
