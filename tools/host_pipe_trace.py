@@ -5,8 +5,9 @@ timeline's summary: run it under rocprofv3, then `host_pipe_trace.py --summarize
 
     rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d D -o run -- python3 tools/host_pipe_trace.py
     python3 tools/host_pipe_trace.py --summarize D
+    python3 tools/host_pipe_trace.py --detail D 40     (the last 40 events with queue / stream ids)
 
-(CHUNK_MIB / OUT_DIRECT in the environment: the pipeline's chunk size and kernel-written outputs.)
+(CHUNK_MIB / OUT_DIRECT in the environment: the pipeline's chunk size and copy mode, default 5.)
 
 The summary takes the last call: per chunk the H2D copy, kernel and D2H copy intervals (us from
 the call's first copy), and the totals: the call's span, each engine's busy time, and the time
@@ -39,7 +40,7 @@ def run(calls: int = 6) -> None:
     L, h = N.lib(), ctx.handle
     if os.environ.get("CHUNK_MIB"):  # pipeline settings under test (cmpi_debug_set_host_chunk / _out_direct)
         L.cmpi_debug_set_host_chunk(int(os.environ["CHUNK_MIB"]) << 20)
-    L.cmpi_debug_set_host_out_direct(int(os.environ.get("OUT_DIRECT", "0")))
+    L.cmpi_debug_set_host_out_direct(int(os.environ.get("OUT_DIRECT", "5")))
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     rates = []
     for _ in range(calls):
@@ -97,8 +98,27 @@ def summarize(d: str) -> None:
                       "kernel_busy_us": round(kern, 1), "both_directions_us": round(both / 1e3, 1)}))
 
 
+def detail(d: str, n: int) -> None:
+    """The last n events of the trace (library kernels, HIP blit kernels, copies) with their queue
+    and stream ids: start, end, duration in us from the first one shown."""
+    def rows(pat):
+        f = glob.glob(os.path.join(d, "**", pat), recursive=True)
+        return list(csv.DictReader(open(f[0]))) if f else []
+
+    ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:40], r.get("Queue_Id", ""),
+           r.get("Stream_Id", "")) for r in rows("*kernel_trace.csv") if "fillBuffer" not in r["Kernel_Name"]]
+    ev += [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "COPY " + r.get("Direction", r.get("Operation", "")),
+            r.get("Queue_Id", ""), r.get("Stream_Id", "")) for r in rows("*memory_copy_trace.csv")]
+    ev.sort()
+    t0 = ev[-n][0]
+    for s, e, name, q, st in ev[-n:]:
+        print(f"{(s - t0) / 1e3:9.1f} {(e - t0) / 1e3:9.1f} {(e - s) / 1e3:7.1f} {name:40s} q={q} s={st}")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--summarize":
         summarize(sys.argv[2])
+    elif len(sys.argv) > 3 and sys.argv[1] == "--detail":
+        detail(sys.argv[2], int(sys.argv[3]))
     else:
         run()
