@@ -1148,6 +1148,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   const size_t slot_b = up2m(in_b + out_b + n_b + st_b + ws_b);
   if (P.cap < slot_b || P.ns < NS) {
     for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
+    if (P.dsig_init)  // (calls return with no copy in flight; this only guards the free below)
+      for (int i = 0; i < 4; ++i) (void)sig_wait_done(P.dsig[i]), (void)sig_wait_done(P.hsig[i]);
     if (P.buf) (void)hipFree(P.buf);
     if (P.hbuf) (void)hipHostFree(P.hbuf);
     P.buf = P.hbuf = nullptr;
@@ -1248,9 +1250,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     }
   }
   if (omode != 1) dout_all = nullptr, dst_all = nullptr;  // mode 1 alone: the kernel writes them
-  auto sdma_wait = [&](int sl) {
-    (void)hsa_signal_wait_scacquire(P.dsig[sl], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
-  };
+  auto sdma_wait = [&](int sl) { return sig_wait_done(P.dsig[sl]) == 0; };
   // D2H of chunk ci by SDMA: wait (spinning) for its kernel, then one copy (+ the statuses)
   auto sdma_d2h = [&](size_t ci, size_t r0, size_t nr) -> int {
     const int sl = (int)(ci % NS);
@@ -1277,9 +1277,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   uint8_t* in_d = ha && omode == 5 && in_flat && n_once ? (uint8_t*)pinned_dev_ptr(in) : nullptr;
   uint8_t* non_d = in_d ? (uint8_t*)pinned_dev_ptr(nonces) : nullptr;
   if (in_d && non_d) {
-    auto sig_ok = [&](hsa_signal_t sg) {
-      return hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) == 0;
-    };
+    auto sig_ok = [&](hsa_signal_t sg) { return sig_wait_done(sg) == 0; };
     // chunks of K records, the last one the remainder (measured and not taken, round 6: a ramp of
     // K/8, K/4, K/2 first to shorten the fill, and each chunk's nonces copied with it instead of
     // the batch's once — 33.9-37.4 against 37.1-37.5 GiB/s, profiles/r06_hostpath_sweeps.jsonl)
@@ -1374,9 +1372,12 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     if (in_rec && !in_pinned) par_copy_records(h.in, ip, in + r0 * in_stride, in_stride, in_rec, nr);
     if (!n_flat)
       for (size_t i = 0; i < nr; ++i) memcpy(h.n + 16 * i, nonces + (r0 + i) * nonce_stride, 12);
-    if (ci >= NS && ha)
-      sdma_wait(sl);  // chunk ci-NS's SDMA copy has read the slot
-    else if (ci >= NS)
+    if (ci >= NS && ha) {  // chunk ci-NS's SDMA copy has read the slot
+      if (!sdma_wait(sl)) {
+        rc = fail(CMPI_EHIP, "chunk %zu output copy failed", ci - NS);
+        break;
+      }
+    } else if (ci >= NS)
       HIP_TRY(hipStreamWaitEvent(sH, P.slot_free[sl], 0));
     // the batch's nonces ahead of chunk 0's records: the first kernel then starts when they land
     if (n_once && ci == 0) HIP_TRY(hipMemcpyAsync(P.dnon, nonces, (nrec - 1) * npitch + 12, hipMemcpyHostToDevice, sH));
@@ -1432,7 +1433,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   }
   if (ha) {
     if (!rc) rc = sdma_d2h(nchunks - 1, (nchunks - 1) * K, nrec - (nchunks - 1) * K);
-    for (size_t i = 0; i < NS; ++i) sdma_wait((int)i);  // every issued copy done (also after an error)
+    for (size_t i = 0; i < NS; ++i)  // every issued copy done (also after an error)
+      if (!sdma_wait((int)i) && !rc) rc = fail(CMPI_EHIP, "output copy failed");
   }
   if (!rc && cpu_unpack) rc = unpack(nchunks - 1);
   for (auto& st : P.s) HIP_TRY(hipStreamSynchronize(st));
@@ -1658,9 +1660,9 @@ void cmpi_ctx_free(cmpi_ctx* c) {
     if (P.hst) (void)hipHostFree(P.hst);
     if (P.dbounce) (void)hipHostFree(P.dbounce);
     if (P.hflag) (void)hipHostFree(P.hflag);
-    if (P.dsig_init) {
-      for (auto& sg : P.dsig) (void)hsa_signal_destroy(sg);
-      for (auto& sg : P.hsig) (void)hsa_signal_destroy(sg);
+    if (P.dsig_init) {  // (every call waits for its copies; a copy is never left to outlive the staging)
+      for (auto& sg : P.dsig) (void)sig_wait_done(sg), (void)hsa_signal_destroy(sg);
+      for (auto& sg : P.hsig) (void)sig_wait_done(sg), (void)hsa_signal_destroy(sg);
     }
   }
   if (c->dt) (void)hipFree(c->dt);

@@ -81,6 +81,17 @@ const HsaAgents& hsa_agents(int dev) {
   return tab[dev];
 }
 
+// Wait until the signal is at most 0 (its copies done; < 0: one failed) and return its value.
+// hsa_signal_wait_* may return before the condition holds, so the observed value is checked: a
+// copy still in flight when the call returned wrote into staging the next allocation reused
+// (round 6: an illegal address in a later test, before this loop).
+hsa_signal_value_t sig_wait_done(hsa_signal_t sg) {
+  hsa_signal_value_t v;
+  while ((v = hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE)) > 0) {
+  }
+  return v;
+}
+
 // An SDMA copy on `eng` (0: the runtime picks the engine).
 hsa_status_t sdma_copy(void* dst, hsa_agent_t da, const void* src, hsa_agent_t sa, size_t n, uint32_t ndep,
                        const hsa_signal_t* deps, hsa_signal_t done, uint32_t eng) {
