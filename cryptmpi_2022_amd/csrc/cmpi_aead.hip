@@ -1280,7 +1280,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     auto sig_ok = [&](hsa_signal_t sg) { return sig_wait_done(sg) == 0; };
     // chunks of K records, the last one the remainder (measured and not taken, round 6: a ramp of
     // K/8, K/4, K/2 first to shorten the fill, and each chunk's nonces copied with it instead of
-    // the batch's once — 33.9-37.4 against 37.1-37.5 GiB/s, profiles/r06_hostpath_sweeps.jsonl)
+    // the batch's once — 33.9-37.4 against 37.1-37.5 GiB/s; each output copy split in 2 or 4
+    // copies — 35.9 / 33.2 against 37.4; profiles/r06_hostpath_sweeps.jsonl)
     std::vector<size_t> cs{0};
     while (cs.back() < nrec) cs.push_back(std::min(nrec, cs.back() + K));
     const size_t nch = cs.size() - 1;
