@@ -576,12 +576,34 @@ def host_path_rate(device: int, n: int = 1024, nrec: int = 65536) -> dict:
             fn()
         return nrec * n / ((time.perf_counter() - t0) / reps) / GIB
 
+    back = registered_host_buffer(nrec * n)
+    st = (ctypes.c_int32 * nrec)()
+
+    def host_open():
+        N.check(L.cmpi_gcm_open_host(h, P(back), n, P(out), n + 16, P(nonces), 12, n, nrec, st))
+
+    def hip_copies():  # the copy mode of rounds 4-5 (hipMemcpyAsync both ways, 16 MiB chunks)
+        L.cmpi_debug_set_host_out_direct(0)
+        L.cmpi_debug_set_host_chunk(16 << 20)
+        try:
+            return round(rate(lambda: host_api(pt, out, nonces)), 2)
+        finally:
+            L.cmpi_debug_set_host_out_direct(5)
+            L.cmpi_debug_set_host_chunk(0)
+
     res = {"config": f"{nrec} x {n} B GCM seal, host buffers in and out",
            "pinned_serial_1stream_GiBps": round(rate(serial), 2),
            "host_api_pinned_pipelined_GiBps": round(rate(lambda: host_api(pt, out, nonces)), 2),
+           "host_api_pinned_open_GiBps": round(rate(host_open), 2),
            "host_api_torch_pin_pipelined_GiBps": round(rate(lambda: host_api(tp_pt, tp_out, tp_n)), 2),
            "host_api_pageable_GiBps": round(rate(lambda: host_api(pg_pt, pg_out, pg_n), 4), 2),
-           "pinned_buffers": "registered_host_buffer (2 MiB aligned, MADV_HUGEPAGE, cmpi_host_register)"}
+           "host_api_pinned_hip_copies_GiBps": hip_copies(),
+           "pinned_buffers": "registered_host_buffer (2 MiB aligned, MADV_HUGEPAGE, cmpi_host_register)",
+           "copy_mode": "both directions on SDMA through HSA, host-launched kernels (cmpi_debug_set_host_out_direct 5); "
+                        "hip_copies: hipMemcpyAsync both ways (mode 0)"}
+    host_api(pt, out, nonces)
+    host_open()
+    res["round_trip"] = bool(torch.equal(back, pt)) and all(x == 1 for x in st)
     ctx.close()
     return res
 
