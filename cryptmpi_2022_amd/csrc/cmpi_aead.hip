@@ -1251,7 +1251,8 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
   }
   if (omode != 1) dout_all = nullptr, dst_all = nullptr;  // mode 1 alone: the kernel writes them
   auto sdma_wait = [&](int sl) { return sig_wait_done(P.dsig[sl]) == 0; };
-  // D2H of chunk ci by SDMA: wait (spinning) for its kernel, then one copy (+ the statuses)
+  // D2H of chunk ci by SDMA: wait (spinning) for its kernel, then one copy (open's statuses the
+  // kernel wrote into the page-locked status array itself: a second copy per chunk cost ~10 us)
   auto sdma_d2h = [&](size_t ci, size_t r0, size_t nr) -> int {
     const int sl = (int)(ci % NS);
     const auto d = layout(sl, P.buf);
@@ -1259,15 +1260,11 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     while ((q = hipEventQuery(P.k_done[sl])) == hipErrorNotReady) {
     }
     if (q != hipSuccess) return fail(CMPI_EHIP, "chunk %zu kernel: %s", ci, hipGetErrorString(q));
-    hsa_signal_store_relaxed(P.dsig[sl], DEC ? 2 : 1);
+    hsa_signal_store_relaxed(P.dsig[sl], 1);
     if (sdma_copy(sd_out + r0 * out_stride, ha->cpu, d.out, ha->gpu, (nr - 1) * op + out_rec, 0, nullptr, P.dsig[sl],
                   ha->eng_d2h) != HSA_STATUS_SUCCESS) {
       hsa_signal_store_relaxed(P.dsig[sl], 0);  // nothing in flight on this slot
       return fail(CMPI_EHIP, "hsa_amd_memory_async_copy (chunk %zu) failed", ci);
-    }
-    if (DEC && sdma_copy(sd_st + r0, ha->cpu, d.st, ha->gpu, 4 * nr, 0, nullptr, P.dsig[sl], ha->eng_d2h) != HSA_STATUS_SUCCESS) {
-      hsa_signal_subtract_relaxed(P.dsig[sl], 1);  // only the record copy is in flight
-      return fail(CMPI_EHIP, "hsa_amd_memory_async_copy (chunk %zu statuses) failed", ci);
     }
     return CMPI_OK;
   };
@@ -1322,8 +1319,9 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
           const size_t r0 = cs[kl], nr = cs[kl + 1] - cs[kl];
           const auto d = layout(sl, P.buf);
           void* wsp = ws_b ? (void*)d.ws : nullptr;
-          rc = OCB ? ocb_batch<DEC>(c, d.out, op, d.in, ip, P.dnon + r0 * npitch, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1])
-                   : gcm_batch<DEC>(c, d.out, op, d.in, ip, P.dnon + r0 * npitch, npitch, len, nr, DEC ? d.st : nullptr, wsp, P.s[1]);
+          int32_t* ks = DEC ? sd_st + r0 : nullptr;  // open's statuses: the kernel writes them to the page-locked array
+          rc = OCB ? ocb_batch<DEC>(c, d.out, op, d.in, ip, P.dnon + r0 * npitch, npitch, len, nr, ks, wsp, P.s[1])
+                   : gcm_batch<DEC>(c, d.out, op, d.in, ip, P.dnon + r0 * npitch, npitch, len, nr, ks, wsp, P.s[1]);
           if (rc) break;
           HIP_TRY(hipEventRecord(P.k_done[sl], P.s[1]));
           ++kl;
@@ -1401,7 +1399,7 @@ int aead_host(const cmpi_ctx* c, uint8_t* out, size_t out_stride, const uint8_t*
     void* wsp = ws_b ? (void*)d.ws : nullptr;
     const uint8_t* dn = n_once ? P.dnon + r0 * npitch : d.n;
     uint8_t* ko = dout_all ? dout_all + r0 * out_stride : d.out;
-    int32_t* ks = DEC ? (dout_all ? dst_all + r0 : d.st) : nullptr;
+    int32_t* ks = DEC ? (dout_all ? dst_all + r0 : ha ? sd_st + r0 : d.st) : nullptr;
     if (OCB)
       rc = ocb_batch<DEC>(c, ko, op, d.in, ip, dn, npitch, len, nr, ks, wsp, sK);
     else
